@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Multi-Krum throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+    torchrun --nproc-per-node N ... bench.py --gpus N     (one rank per GPU)
+
+One step = one full Multi-Krum pass of the hot path over one synthetic batch
+already resident in HBM: fp64-MFMA Gram (+ RCCL all-reduce of the packed
+partial Gram when N > 1) -> distance rows -> per-row sort and sum of the
+n-f-2 nearest -> selection of the n-f lowest -> masked mean.  The default
+workload is BASELINE.json's headline config, 512 fp64 updates x 1,048,576
+dims, f = 153, with the dimension sharded over the N
+ranks (strong scaling: the batch is fixed, each rank owns d/N columns).
+
+value = n * d * 8 bytes / (max-over-ranks wall time per step), in GB/s.
+rank 0 prints ONE JSON line; see DESIGN.md "Measurement" for every field.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+SEED0 = 20261015
+WORKLOADS = {
+    # BASELINE.json configs; D is the headline
+    "D_512x1M_f153": dict(n=512, d=1048576, f=153, seed=SEED0 + 4, nbyz=153, dtype="f64"),
+    "D_512x1M_f256": dict(n=512, d=1048576, f=256, seed=SEED0 + 4, nbyz=153, dtype="f64"),
+    "C_1024x131072": dict(n=1024, d=131072, f=307, seed=SEED0 + 3, nbyz=307, dtype="f64"),
+    "B_mnist": dict(n=100, d=7850, f=30, seed=SEED0 + 2, nbyz=30, dtype="f64", flags=1),
+    "E_4096x262144_fp32": dict(n=4096, d=262144, f=1228, seed=SEED0 + 5, nbyz=1228, dtype="f32"),
+}
+DEFAULT_WORKLOAD = "D_512x1M_f153"
+METRIC = "Multi-Krum GB/s (device-resident, n fp64 updates x d) + selected-set parity"
+# MI355X dense peaks (MI355X_MICROARCH.md chip table / spec): fp64 matrix 78.6 TF/s,
+# fp32 matrix 157.3 TF/s, HBM3E 8 TB/s
+PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(w, target_s=12.0):
+    """Time the oracle (C/OpenMP restatement of the reference's numpy krum,
+    oracle/krum_oracle.c) on a bounded column sample of the same batch."""
+    from oracle import oracle as O
+    n, d, f = w["n"], w["d"], w["f"]
+    dt = np.float32 if w["dtype"] == "f32" else np.float64
+    es = 4 if w["dtype"] == "f32" else 8
+
+    def run(ds):
+        X = O.synth(n, d, w["seed"], w["nbyz"], flags=w.get("flags", 0), dtype=dt, c0=0, dl=ds,
+                    d_total=d)
+        t0 = time.perf_counter()
+        O.krum(X, f)
+        return time.perf_counter() - t0
+
+    ds = min(d, 32768)
+    t = run(ds)
+    if t < target_s / 4 and ds < d:
+        ds2 = int(min(d, ds * max(1.0, target_s / max(t, 1e-3))))
+        ds2 = max(8, ds2 // 8 * 8)
+        if ds2 > ds:
+            ds, t = ds2, run(ds2)
+    return {"value": round(n * ds * es / t / 1e9, 4), "unit": "GB/s", "cores": O.num_threads(),
+            "kind": "port",
+            "sample": "oracle/krum_oracle.c (OpenMP) full Multi-Krum (Gram, sort, select, mean) "
+                      "on the first %d of %d columns of the same %dx%d batch, %.2f s" %
+                      (ds, d, n, d, t)}
+
+
+def golden_check(name, sel_host, mean_local, c0, dl):
+    path = os.path.join(REPO, "tests", "golden", name + ".npz")
+    if not os.path.exists(path):
+        return None
+    g = np.load(path, allow_pickle=False)
+    ok = bool(np.array_equal(np.sort(sel_host), g["sel"]))
+    res = {"selected_set": "match" if ok else "MISMATCH"}
+    if "mean_cols" in g.files and mean_local is not None:
+        cols = g["mean_cols"]
+        msk = (cols >= c0) & (cols < c0 + dl)
+        if msk.any():
+            man = json.load(open(os.path.join(REPO, "tests", "golden", "cases.json")))
+            scale = man[name]["mean_scale"]
+            err = float(np.max(np.abs(mean_local[cols[msk] - c0] - g["mean_vals"][msk])))
+            res["mean_max_err_rel"] = err / scale
+            res["mean"] = "match" if err <= 1e-9 * scale else "MISMATCH"
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default=DEFAULT_WORKLOAD, choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="multi-GPU: all-gather + fixed-order sum instead of all-reduce")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, a.gpus))
+
+    import torch
+    import torch.distributed as tdist
+
+    from biscotti_amd import _lib
+    from biscotti_amd.dist import bootstrap_rccl, shard_bounds, torch_broadcast_bytes
+    from biscotti_amd.krum import Engine
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        tdist.init_process_group("nccl", device_id=dev)
+
+    w = WORKLOADS[a.workload]
+    n, d, f = w["n"], w["d"], w["f"]
+    m = n - f
+    c0, dl = shard_bounds(d, world, rank)
+    tdt = torch.float32 if w["dtype"] == "f32" else torch.float64
+    bdt = _lib.BK_F32 if w["dtype"] == "f32" else _lib.BK_F64
+    es = 4 if w["dtype"] == "f32" else 8
+
+    eng = Engine(local_rank)
+    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    if world > 1:
+        bootstrap_rccl(eng, rank, world, torch_broadcast_bytes)
+        eng.comm_set_mode(a.deterministic)
+
+    X = torch.empty((n, max(dl, 1)), dtype=tdt, device=dev)
+    eng.synth_fill_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), c0, d, w["seed"], w["nbyz"],
+                       flags=w.get("flags", 0))
+    sel = torch.empty(m, dtype=torch.int64, device=dev)
+    scores = torch.empty(n, dtype=torch.float64, device=dev)
+    mean = torch.empty(max(dl, 1), dtype=torch.float64, device=dev)
+
+    def step():
+        if world == 1:
+            eng.multikrum_device_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f, sel.data_ptr(),
+                                     scores.data_ptr(), mean.data_ptr())
+        else:
+            eng.multikrum_sharded_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f, sel.data_ptr(),
+                                      scores.data_ptr(), mean.data_ptr())
+
+    def barrier():
+        if world > 1:
+            tdist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    eng.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    kt = eng.timing_read()
+    eng.timing_enable(False)
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed / a.steps * 1e3
+    value = n * d * es / (elapsed / a.steps) / 1e9
+
+    parity = golden_check(a.workload, sel.cpu().numpy(), mean[:dl].cpu().numpy(), c0, dl)
+
+    # roofline of the dominant kernel (K1, fp64 MFMA): algorithmic flops per
+    # launch = n(n+1) * d_local (symmetric Gram incl. diagonal)
+    g = kt.get("k_gram", {"avg_ms": float("nan")})
+    flops = n * (n + 1) * dl
+    achieved = flops / (g["avg_ms"] * 1e-3) / 1e12
+    peak = PEAK_TFLOPS["f64"]  # fp32 inputs are widened onto the fp64 MFMA path
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "pmc_%s.json" % a.workload)
+    if os.path.exists(pmc_path) and world == 1:
+        try:
+            traffic = json.load(open(pmc_path)).get("k_gram", {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "kernel": "k_gram", "kernel_avg_ms": round(g["avg_ms"], 4),
+            "flops_per_launch": flops}
+
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": w["dtype"],
+        "data": "synthetic (repo SplitMix64 spec, generated on device; DESIGN.md)",
+        "config": {"workload": a.workload, "n": n, "d": d, "f": f, "m": m,
+                   "parallelism": "d-shard x%d + RCCL all-reduce" % world if world > 1 else "1 GPU",
+                   "d_local": dl},
+        "roofline": roof,
+        "kernels_ms_avg": {k: round(v["avg_ms"], 5) for k, v in kt.items()},
+        "parity": parity,
+    }
+
+    if rank == 0 and world == 1 and not a.no_e2e:
+        # PCIe-inclusive rate: pinned host batch -> H2D -> Multi-Krum -> D2H of sel and mean
+        import ctypes
+        Xh = torch.empty((n, dl), dtype=tdt, pin_memory=True)
+        Xh.copy_(X[:, :dl])
+        selh = np.empty(m, dtype=np.int64)
+        meanh = np.empty(dl, dtype=np.float64)
+        mo = ctypes.c_int64(0)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _lib.check(_lib.lib().bk_multikrum(eng.ctx, ctypes.c_void_p(Xh.data_ptr()),
+                                               _lib.BK_HOST_PINNED, bdt, n, dl, dl, f,
+                                               selh.ctypes.data, ctypes.addressof(mo), None,
+                                               meanh.ctypes.data))
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        out["e2e_pinned_h2d_d2h"] = {"GB_per_s": round(n * d * es / t / 1e9, 3),
+                                     "ms": round(t * 1e3, 3),
+                                     "selected_set_same": bool(np.array_equal(
+                                         selh, sel.cpu().numpy()))}
+        del Xh
+
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(w)
+        except Exception as e:  # the oracle is optional for the GPU number itself
+            out["cpu_baseline"] = {"error": repr(e)}
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        tdist.barrier()
+        tdist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,58 @@
+"""Build recipe for libbk.so (the HIP engine + C ABI), gfx950 only.
+
+    python -m biscotti_amd.build            # or __graft_entry__.build()
+
+hipcc cross-compiles without a GPU.  The .so lands in-tree
+(biscotti_amd/libbk.so) so it travels to the GPU box with the repo snapshot.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libbk.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+
+SOURCES = ["bk_kernels.hip", "bk_api.hip"]
+FLAGS = [
+    "--offload-arch=gfx950",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    # the synthetic generator and the distance / mean arithmetic must round
+    # exactly like numpy (no implicit FMA); MFMA is explicit
+    "-ffp-contract=off",
+    "-Wall",
+    "-Wno-unused-function",
+    "-I" + os.path.join(REPO, "include"),
+    "-I" + CSRC,
+]
+LIBS = ["-L" + os.path.join(ROCM, "lib"), "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib")]
+
+
+def needs_build():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(REPO, "include", "bk.h"),
+                                                                 __file__]
+    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+
+
+def build(force=False, verbose=True, extra=()):
+    if not force and not needs_build():
+        return LIB
+    cmd = [HIPCC] + FLAGS + list(extra) + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB + ".tmp"] + LIBS
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,625 @@
+// bk_api.hip -- the C ABI (include/bk.h): context, workspace, orchestration,
+// RCCL exchange, per-kernel HIP-event timing.  No torch, no C++ types across
+// the boundary; every failure becomes a negative status + bk_last_error().
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/bk.h"
+#include "bk_internal.h"
+#include "bk_synth.h"
+
+using namespace bk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return fail(_e == hipErrorOutOfMemory ? BK_ENOMEM : BK_EHIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(_e), __FILE__, __LINE__);                \
+    } while (0)
+
+#define RCCLCHK(expr)                                                                        \
+    do {                                                                                     \
+        ncclResult_t _r = (expr);                                                            \
+        if (_r != ncclSuccess)                                                               \
+            return fail(BK_ERCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(_r), __FILE__, \
+                        __LINE__);                                                           \
+    } while (0)
+
+#define CHK(expr)              \
+    do {                       \
+        int _s = (expr);       \
+        if (_s != BK_OK) return _s; \
+    } while (0)
+
+const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_expand", "k_scores",
+                                            "k_rank",    "k_compact", "k_mean",   "allreduce",
+                                            "k_synth",   "h2d",       "d2h"};
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct bk_ctx {
+    int device = 0;
+    int num_cu = 256;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // workspace (grow-only)
+    DevBuf part, U, Ug, G, diag, scores, mask, sel, X, mean, perm;
+    // host-side pinned allocations handed out by bk_stage_alloc
+    std::vector<void *> staged;
+    // timing
+    bool timing = false;
+    struct Ev {
+        int kid;
+        hipEvent_t a, b;
+    };
+    std::vector<Ev> pending;
+    std::vector<hipEvent_t> pool;
+    double tot_ms[BK_NUM_KERNELS] = {0};
+    int64_t cnt[BK_NUM_KERNELS] = {0};
+    // RCCL
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    int deterministic = 0;
+};
+
+namespace {
+
+int ensure(DevBuf &b, size_t bytes) {
+    if (bytes <= b.bytes) return BK_OK;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+        if (e != hipSuccess) return fail(BK_EHIP, "hipFree: %s", hipGetErrorString(e));
+    }
+    size_t want = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return fail(BK_ENOMEM, "hipMalloc(%zu bytes): %s", want, hipGetErrorString(e));
+    }
+    b.bytes = want;
+    return BK_OK;
+}
+
+int get_event(bk_ctx *c, hipEvent_t *out) {
+    if (!c->pool.empty()) {
+        *out = c->pool.back();
+        c->pool.pop_back();
+        return BK_OK;
+    }
+    HIPCHK(hipEventCreate(out));
+    return BK_OK;
+}
+
+// Bracket one launch with events when timing is on.
+template <typename F>
+int timed(bk_ctx *c, int kid, F &&launch) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->timing) {
+        CHK(get_event(c, &a));
+        CHK(get_event(c, &b));
+        HIPCHK(hipEventRecord(a, c->stream));
+    }
+    hipError_t e = launch();
+    if (e != hipSuccess)
+        return fail(BK_EHIP, "%s launch: %s", kKernelNames[kid], hipGetErrorString(e));
+    if (c->timing) {
+        HIPCHK(hipEventRecord(b, c->stream));
+        c->pending.push_back({kid, a, b});
+    }
+    return BK_OK;
+}
+
+
+Plan make_plan(int64_t n, int64_t d, int num_cu, size_t in_bytes) {
+    Plan pl;
+    pl.n = (int)n;
+    pl.d = d;
+    pl.T = (int)((n + 63) / 64);
+    pl.ntile = pl.T * (pl.T + 1) / 2;
+    const int64_t W = (int64_t)num_cu * 4;  // one wave per SIMD (K1 runs 1 workgroup per CU)
+    const size_t part_cap = in_bytes / 16 > (64u << 20) ? in_bytes / 16 : (64u << 20);
+    double best_cost = 1e300;
+    int best_S = 1;
+    for (int S = 1; S <= 4096; ++S) {
+        const int64_t kc = ((d + S - 1) / S + 7) / 8 * 8;
+        if (S > 1 && kc < 256) break;
+        const int64_t Se = (d + kc - 1) / kc;
+        if (Se != S) continue;
+        if (S > 1 && (size_t)pl.ntile * S * 32768 > part_cap) break;
+        const int64_t tasks = (int64_t)pl.ntile * S;
+        const int64_t rounds = (tasks + W - 1) / W;
+        const double cost = (double)rounds * (double)(kc + 64);  // +64: per-task fixed cost
+        if (cost < best_cost * 0.99) {
+            best_cost = cost;
+            best_S = S;
+        }
+    }
+    pl.S = best_S;
+    pl.kc = ((d + best_S - 1) / best_S + 7) / 8 * 8;
+    const int64_t tasks = (int64_t)pl.ntile * pl.S;
+    pl.nwg = (int)((tasks + 3) / 4);
+    return pl;
+}
+
+int check_common(bk_ctx *c, const void *X, int dtype, int64_t n, int64_t d, int64_t ld) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    if (!X) return fail(BK_EINVAL, "null X");
+    if (dtype != BK_F64 && dtype != BK_F32) return fail(BK_EINVAL, "bad dtype %d", dtype);
+    if (n < 1 || d < 1) return fail(BK_EINVAL, "need n >= 1 and d >= 1 (n=%lld d=%lld)",
+                                   (long long)n, (long long)d);
+    if (n > BK_MAX_N) return fail(BK_ENOTSUP, "n=%lld exceeds BK_MAX_N=%d", (long long)n, BK_MAX_N);
+    if (ld < d) return fail(BK_EINVAL, "ld=%lld < d=%lld", (long long)ld, (long long)d);
+    return BK_OK;
+}
+
+size_t esize(int dtype) { return dtype == BK_F64 ? 8 : 4; }
+
+// K1 + K1b: packed upper-triangle Gram of this call's columns into U
+int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
+               double *U, Plan &pl) {
+    pl = make_plan(n, d, c->num_cu, (size_t)n * d * esize(dtype));
+    CHK(ensure(c->part, (size_t)pl.ntile * pl.S * 4096 * sizeof(double)));
+    double *part = (double *)c->part.p;
+    CHK(timed(c, BK_K_GRAM,
+              [&] { return launch_gram(dX, dtype, ld, (int)n, d, pl, part, c->stream); }));
+    CHK(timed(c, BK_K_REDUCE, [&] { return launch_reduce(part, pl, U, c->stream); }));
+    return BK_OK;
+}
+
+// K1c + K2 + K3 + K4 from a packed upper Gram
+int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int dtype,
+                 int64_t n, int64_t d, int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
+                 double *d_mean) {
+    CHK(ensure(c->G, (size_t)n * n * sizeof(double)));
+    CHK(ensure(c->diag, (size_t)n * sizeof(double)));
+    CHK(ensure(c->mask, (size_t)n * sizeof(int)));
+    double *sc = d_scores;
+    if (!sc) {
+        CHK(ensure(c->scores, (size_t)n * sizeof(double)));
+        sc = (double *)c->scores.p;
+    }
+    double *G = (double *)c->G.p, *diag = (double *)c->diag.p;
+    int *mask = (int *)c->mask.p;
+    const int64_t m = n - f;
+    const int64_t k = n - f - 2 > 0 ? n - f - 2 : 0;
+    CHK(timed(c, BK_K_EXPAND,
+              [&] { return launch_expand(U, (int)n, pl.T, pl.ntile, G, diag, c->stream); }));
+    CHK(timed(c, BK_K_SCORES, [&] { return launch_scores(G, diag, (int)n, k, sc, c->stream); }));
+    CHK(timed(c, BK_K_RANK, [&] { return launch_rank(sc, (int)n, (int)m, mask, c->stream); }));
+    CHK(timed(c, BK_K_COMPACT, [&] { return launch_compact(mask, (int)n, d_sel, c->stream); }));
+    if (d_mean && d > 0)
+        CHK(timed(c, BK_K_MEAN, [&] {
+            return launch_mean(dX, dtype, ld, d, d_sel, (int)m, d_mean, c->num_cu, c->stream);
+        }));
+    return BK_OK;
+}
+
+int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld, int64_t f,
+               int64_t *d_sel, double *d_scores, double *d_mean) {
+    Plan pl;
+    const size_t usz = (size_t)((n + 63) / 64) * ((n + 63) / 64 + 1) / 2 * 4096;
+    CHK(ensure(c->U, usz * sizeof(double)));
+    double *U = (double *)c->U.p;
+    CHK(stage_gram(c, dX, dtype, n, d, ld, U, pl));
+    return stage_finish(c, U, pl, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int bk_abi_version(void) { return BK_ABI_VERSION; }
+
+const char *bk_last_error(void) { return g_err.c_str(); }
+
+int bk_check_args(int64_t n, int64_t d, int64_t f) {
+    if (n < 1 || d < 1) return fail(BK_EINVAL, "need n >= 1 and d >= 1");
+    if (f < 1 || f >= n)
+        return fail(BK_EINVAL, "need 1 <= f < n (n=%lld f=%lld); f=0 is the reference's "
+                               "argpartition ValueError",
+                    (long long)n, (long long)f);
+    if (n > BK_MAX_N) return fail(BK_ENOTSUP, "n=%lld exceeds BK_MAX_N=%d", (long long)n, BK_MAX_N);
+    return BK_OK;
+}
+
+const char *bk_kernel_name(int kid) {
+    return (kid >= 0 && kid < BK_NUM_KERNELS) ? kKernelNames[kid] : "?";
+}
+
+int64_t bk_upper_elems(int64_t n) {
+    const int64_t T = (n + 63) / 64;
+    return T * (T + 1) / 2 * 4096;
+}
+
+int bk_create(bk_ctx **out, int device) {
+    if (!out) return fail(BK_EINVAL, "null out");
+    *out = nullptr;
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev)
+        return fail(BK_EINVAL, "device %d out of range (%d visible)", device, ndev);
+    bk_ctx *c = new (std::nothrow) bk_ctx();
+    if (!c) return fail(BK_ENOMEM, "host allocation of bk_ctx failed");
+    c->device = device;
+    DeviceGuard dg(device);
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e == hipSuccess) c->num_cu = prop.multiProcessorCount;
+    e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(BK_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    c->stream = c->own;
+    e = configure_kernels();
+    if (e != hipSuccess) {
+        (void)hipStreamDestroy(c->own);
+        delete c;
+        return fail(BK_EHIP, "configure_kernels: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return BK_OK;
+}
+
+void bk_destroy(bk_ctx *c) {
+    if (!c) return;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        DeviceGuard dg(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->G,    &c->diag, &c->scores,
+                          &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm};
+        for (DevBuf *b : bufs)
+            if (b->p) (void)hipFree(b->p);
+        for (void *p : c->staged) (void)hipHostFree(p);
+        for (auto &ev : c->pending) {
+            (void)hipEventDestroy(ev.a);
+            (void)hipEventDestroy(ev.b);
+        }
+        for (hipEvent_t ev : c->pool) (void)hipEventDestroy(ev);
+        if (c->comm) (void)ncclCommDestroy(c->comm);
+        if (c->own) (void)hipStreamDestroy(c->own);
+    }
+    delete c;
+}
+
+int bk_set_stream(bk_ctx *c, void *s) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->stream = s ? (hipStream_t)s : c->own;
+    return BK_OK;
+}
+
+void *bk_get_stream(bk_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int bk_synchronize(bk_ctx *c) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BK_OK;
+}
+
+int bk_stage_alloc(bk_ctx *c, int64_t bytes, void **pinned) {
+    if (!c || !pinned || bytes <= 0) return fail(BK_EINVAL, "bad stage_alloc arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(BK_ENOMEM, "hipHostMalloc(%lld): %s", (long long)bytes,
+                                     hipGetErrorString(e));
+    c->staged.push_back(p);
+    *pinned = p;
+    return BK_OK;
+}
+
+int bk_stage_free(bk_ctx *c, void *p) {
+    if (!c || !p) return fail(BK_EINVAL, "bad stage_free arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (size_t i = 0; i < c->staged.size(); ++i) {
+        if (c->staged[i] == p) {
+            c->staged.erase(c->staged.begin() + i);
+            HIPCHK(hipHostFree(p));
+            return BK_OK;
+        }
+    }
+    return fail(BK_EINVAL, "pointer was not allocated by bk_stage_alloc");
+}
+
+int bk_plan(bk_ctx *c, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *ntile,
+            int64_t *nwg) {
+    if (n < 1 || d < 1) return fail(BK_EINVAL, "need n, d >= 1");
+    const Plan pl = make_plan(n, d, c ? c->num_cu : 256, (size_t)n * d * 8);
+    if (S) *S = pl.S;
+    if (kc) *kc = pl.kc;
+    if (ntile) *ntile = pl.ntile;
+    if (nwg) *nwg = pl.nwg;
+    return BK_OK;
+}
+
+int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
+                        int64_t f, int64_t *d_sel, double *d_scores, double *d_mean) {
+    CHK(check_common(c, dX, dtype, n, d, ld));
+    CHK(bk_check_args(n, d, f));
+    if (!d_sel) return fail(BK_EINVAL, "null d_sel_idx");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
+}
+
+int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int64_t d, int64_t ld,
+                 int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores, double *mean_out) {
+    CHK(check_common(c, X, dtype, n, d, ld));
+    CHK(bk_check_args(n, d, f));
+    if (!sel_idx) return fail(BK_EINVAL, "null sel_idx");
+    if (where != BK_HOST && where != BK_HOST_PINNED && where != BK_DEVICE)
+        return fail(BK_EINVAL, "bad where=%d", where);
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    const size_t es = esize(dtype);
+    const void *dX = X;
+    int64_t dld = ld;
+    if (where != BK_DEVICE) {
+        CHK(ensure(c->X, (size_t)n * d * es));
+        dld = d;
+        void *dst = c->X.p;
+        CHK(timed(c, BK_K_H2D, [&] {
+            if (ld == d) return hipMemcpyAsync(dst, X, (size_t)n * d * es, hipMemcpyHostToDevice,
+                                               c->stream);
+            return hipMemcpy2DAsync(dst, (size_t)d * es, X, (size_t)ld * es, (size_t)d * es,
+                                    (size_t)n, hipMemcpyHostToDevice, c->stream);
+        }));
+        dX = dst;
+    }
+    const int64_t m = n - f;
+    CHK(ensure(c->sel, (size_t)n * sizeof(int64_t)));
+    CHK(ensure(c->scores, (size_t)n * sizeof(double)));
+    if (mean_out) CHK(ensure(c->mean, (size_t)d * sizeof(double)));
+    int64_t *dsel = (int64_t *)c->sel.p;
+    double *dsc = (double *)c->scores.p;
+    double *dmean = mean_out ? (double *)c->mean.p : nullptr;
+    CHK(run_device(c, dX, dtype, n, d, dld, f, dsel, dsc, dmean));
+    CHK(timed(c, BK_K_D2H, [&] {
+        hipError_t e = hipMemcpyAsync(sel_idx, dsel, (size_t)m * sizeof(int64_t),
+                                      hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess && scores)
+            e = hipMemcpyAsync(scores, dsc, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream);
+        if (e == hipSuccess && mean_out)
+            e = hipMemcpyAsync(mean_out, dmean, (size_t)d * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream);
+        return e;
+    }));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (m_out) *m_out = m;
+    return BK_OK;
+}
+
+int bk_gram_upper_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
+                         double *d_upper) {
+    CHK(check_common(c, dX, dtype, n, d, ld));
+    if (!d_upper) return fail(BK_EINVAL, "null d_upper");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    Plan pl;
+    return stage_gram(c, dX, dtype, n, d, ld, d_upper, pl);
+}
+
+int bk_finish_device(bk_ctx *c, const double *d_upper, const void *dX, int dtype, int64_t n,
+                     int64_t d, int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
+                     double *d_mean) {
+    if (d_mean) CHK(check_common(c, dX, dtype, n, d, ld));
+    if (!c) return fail(BK_EINVAL, "null context");
+    CHK(bk_check_args(n, d < 1 ? 1 : d, f));
+    if (!d_upper || !d_sel) return fail(BK_EINVAL, "null d_upper / d_sel_idx");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    Plan pl;
+    pl.n = (int)n;
+    pl.T = (int)((n + 63) / 64);
+    pl.ntile = pl.T * (pl.T + 1) / 2;
+    return stage_finish(c, d_upper, pl, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
+}
+
+int bk_comm_unique_id(void *id_out) {
+    if (!id_out) return fail(BK_EINVAL, "null id");
+    static_assert(sizeof(ncclUniqueId) == BK_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    RCCLCHK(ncclGetUniqueId(&id));
+    memcpy(id_out, &id, sizeof id);
+    return BK_OK;
+}
+
+int bk_comm_init(bk_ctx *c, int nranks, int rank, const void *id) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(BK_EINVAL, "bad comm_init arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    if (c->comm) {
+        (void)ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof uid);
+    RCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return BK_OK;
+}
+
+int bk_comm_set_mode(bk_ctx *c, int deterministic) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    c->deterministic = deterministic ? 1 : 0;
+    return BK_OK;
+}
+
+int bk_multikrum_sharded_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl,
+                                int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
+                                double *d_mean) {
+    CHK(check_common(c, dX, dtype, n, dl, ld));
+    CHK(bk_check_args(n, dl, f));
+    if (!d_sel) return fail(BK_EINVAL, "null d_sel_idx");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    if (c->nranks > 1 && !c->comm) return fail(BK_ERCCL, "bk_comm_init not called");
+    const int64_t usz = bk_upper_elems(n);
+    CHK(ensure(c->U, (size_t)usz * sizeof(double)));
+    double *U = (double *)c->U.p;
+    Plan pl;
+    CHK(stage_gram(c, dX, dtype, n, dl, ld, U, pl));
+    if (c->nranks > 1) {
+        if (!c->deterministic) {
+            hipEvent_t a = nullptr, b = nullptr;
+            if (c->timing) {
+                CHK(get_event(c, &a));
+                CHK(get_event(c, &b));
+                HIPCHK(hipEventRecord(a, c->stream));
+            }
+            RCCLCHK(ncclAllReduce(U, U, (size_t)usz, ncclDouble, ncclSum, c->comm, c->stream));
+            if (c->timing) {
+                HIPCHK(hipEventRecord(b, c->stream));
+                c->pending.push_back({BK_K_ALLREDUCE, a, b});
+            }
+        } else {
+            CHK(ensure(c->Ug, (size_t)usz * c->nranks * sizeof(double)));
+            double *Ug = (double *)c->Ug.p;
+            hipEvent_t a = nullptr, b = nullptr;
+            if (c->timing) {
+                CHK(get_event(c, &a));
+                CHK(get_event(c, &b));
+                HIPCHK(hipEventRecord(a, c->stream));
+            }
+            RCCLCHK(ncclAllGather(U, Ug, (size_t)usz, ncclDouble, c->comm, c->stream));
+            HIPCHK(launch_sum_ranks(Ug, c->nranks, usz, U, c->stream));
+            if (c->timing) {
+                HIPCHK(hipEventRecord(b, c->stream));
+                c->pending.push_back({BK_K_ALLREDUCE, a, b});
+            }
+        }
+    }
+    return stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, d_mean);
+}
+
+int bk_synth_fill_device(bk_ctx *c, void *dX, int dtype, int64_t n, int64_t dl, int64_t ld,
+                         int64_t c0, int64_t d_total, uint64_t seed, int64_t nbyz, double mu_scale,
+                         double byz_scale, double sigma, int flags) {
+    CHK(check_common(c, dX, dtype, n, dl, ld));
+    if (c0 < 0 || c0 + dl > d_total || nbyz < 0 || nbyz > n)
+        return fail(BK_EINVAL, "bad synth column range / nbyz");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    // Fisher-Yates on the host (sequential by definition), then upload
+    std::vector<int64_t> perm((size_t)n);
+    const uint64_t b3 = stream_base(seed, 3);
+    for (int64_t i = 0; i < n; ++i) perm[(size_t)i] = i;
+    for (int64_t i = n - 1; i >= 1; --i) {
+        const int64_t j = (int64_t)(sm64(b3 + (uint64_t)i) % (uint64_t)(i + 1));
+        const int64_t t = perm[(size_t)i];
+        perm[(size_t)i] = perm[(size_t)j];
+        perm[(size_t)j] = t;
+    }
+    CHK(ensure(c->perm, (size_t)n * sizeof(int64_t)));
+    HIPCHK(hipMemcpyAsync(c->perm.p, perm.data(), (size_t)n * sizeof(int64_t),
+                          hipMemcpyHostToDevice, c->stream));
+    SynthParams P;
+    P.b0 = stream_base(seed, 0);
+    P.b1 = stream_base(seed, 1);
+    P.b2 = stream_base(seed, 2);
+    P.b4 = stream_base(seed, 4);
+    P.n = n;
+    P.nbyz = nbyz;
+    P.d_total = d_total;
+    P.mu_scale = mu_scale;
+    P.byz_scale = byz_scale;
+    P.sigma = sigma;
+    P.flags = flags;
+    const int64_t *dperm = (const int64_t *)c->perm.p;
+    CHK(timed(c, BK_K_SYNTH,
+              [&] { return launch_synth(dX, dtype, ld, n, dl, c0, dperm, P, c->stream); }));
+    // the host perm vector dies here: make sure the (pageable) copy has landed
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BK_OK;
+}
+
+int bk_timing_enable(bk_ctx *c, int on) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (auto &ev : c->pending) {
+        c->pool.push_back(ev.a);
+        c->pool.push_back(ev.b);
+    }
+    c->pending.clear();
+    for (int i = 0; i < BK_NUM_KERNELS; ++i) {
+        c->tot_ms[i] = 0;
+        c->cnt[i] = 0;
+    }
+    c->timing = on != 0;
+    return BK_OK;
+}
+
+int bk_timing_read(bk_ctx *c, int kid, double *total_ms, int64_t *count) {
+    if (!c || kid < 0 || kid >= BK_NUM_KERNELS) return fail(BK_EINVAL, "bad timing_read arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    if (!c->pending.empty()) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (auto &ev : c->pending) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, ev.a, ev.b));
+            c->tot_ms[ev.kid] += ms;
+            c->cnt[ev.kid] += 1;
+            c->pool.push_back(ev.a);
+            c->pool.push_back(ev.b);
+        }
+        c->pending.clear();
+    }
+    if (total_ms) *total_ms = c->tot_ms[kid];
+    if (count) *count = c->cnt[kid];
+    return BK_OK;
+}
+
+}  // extern "C"

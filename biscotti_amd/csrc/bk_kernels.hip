@@ -1,0 +1,571 @@
+// bk_kernels.hip -- CDNA4 (gfx950) kernels of the Multi-Krum engine.
+//
+// Pipeline for one Multi-Krum call (DESIGN.md "Kernels"):
+//   K1  k_gram      split-K, upper-triangle fp64 Gram partials on
+//                   v_mfma_f64_16x16x4_f64 (the -2XX^T term of
+//                   logistic_validator.py:59-60; norms come from its diagonal)
+//   K1b k_reduce    fixed-order sum of the split-K partials -> packed upper
+//   K1c k_expand    packed upper -> symmetric G (n x n) + diag
+//   K2  k_scores    per row: D_ij = (G_ii + G_jj) - 2 G_ij, bitonic sort in LDS
+//                   (NaN last), sum of ranks 1..k      (logistic_validator.py:62-63)
+//   K3  k_rank      rank of each score (ties -> lower index, NaN last), mask
+//   K3b k_compact   mask -> ascending selected indices (argpartition set, :45)
+//   K4  k_mean      masked mean of the selected rows, fp64, ascending order (:51)
+//
+// Built with -ffp-contract=off: every non-MFMA add/mul rounds exactly as the
+// numpy reference evaluates it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+#include "bk_internal.h"
+#include "bk_synth.h"
+
+namespace bk {
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+
+// Bijective XCD remap (cdna_hip_programming.md T1): blocks b and b+8 share an
+// XCD, so give each XCD a contiguous range of logical workgroups.  Speed only.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// upper-triangle sub-tile u -> (bi, bj), bi <= bj, T blocks per side
+__device__ __forceinline__ void tri_decode(int u, int T, int &bi, int &bj) {
+    int i = 0, off = 0;
+    while (u >= off + (T - i)) { off += T - i; ++i; }
+    bi = i;
+    bj = i + (u - off);
+}
+
+// total order on doubles for sorting / selection: ascending, +0 == -0, NaN last
+__device__ __forceinline__ uint64_t dkey(double v) {
+    if (v != v) return 0xFFF8000000000000ULL;
+    if (v == 0.0) v = 0.0;
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double dkey_inv(uint64_t k) {
+    const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
+    return __longlong_as_double((long long)b);
+}
+
+template <typename T, bool VEC>
+__device__ __forceinline__ d2v ld2(const T *p) {
+    d2v r;
+    if constexpr (std::is_same<T, double>::value) {
+        if constexpr (VEC) {
+            r = *reinterpret_cast<const d2v *>(p);
+        } else {
+            r.x = p[0];
+            r.y = p[1];
+        }
+    } else {
+        if constexpr (VEC) {
+            const f2v v = *reinterpret_cast<const f2v *>(p);
+            r.x = (double)v.x;
+            r.y = (double)v.y;
+        } else {
+            r.x = (double)p[0];
+            r.y = (double)p[1];
+        }
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// K1: split-K upper-triangle Gram on fp64 MFMA.
+//
+// One WAVE owns one task = (64x64 upper sub-tile u, k-piece s).  No LDS, no
+// barriers: fp64 MFMA is 64 cycles per 16x16x4 on gfx950, so a wave's 16
+// accumulators hide everything if operands arrive from a register ring P
+// k-blocks deep.  The contraction index is permuted inside each 8-column
+// k-block so that every lane loads 16 contiguous bytes per row:
+//   lane l (rr = l&15, g = l>>4) holds X[row rr][kb*8 + 2g + s] for MFMA
+//   sub-step s in {0,1}; A and B use the same permutation, so the product is
+//   exactly X X^T (the order of the k-sum is a free choice, as in any BLAS).
+// Output: acc[a][b] is the 16x16 block (a,b) of the sub-tile; element
+// (row g + 4r, col rr) sits in register r (f64 MFMA C/D map,
+// cdna_hip_programming.md §3).
+// ---------------------------------------------------------------------------
+
+template <typename T, bool VEC, bool DIAG>
+__device__ __forceinline__ void gram_load(const T *(&pa)[4], const T *(&pb)[4],
+                                          int64_t off, d2v (&a)[4], d2v (&b)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = ld2<T, VEC>(pa[i] + off);
+    if constexpr (!DIAG) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = ld2<T, VEC>(pb[j] + off);
+    }
+}
+
+template <bool DIAG>
+__device__ __forceinline__ void gram_mma(d4v (&acc)[4][4], const d2v (&a)[4], const d2v (&b)[4]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (DIAG && j < i) continue;
+                const double bv = DIAG ? a[j][s] : b[j][s];
+                acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][s], bv, acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+}
+
+template <typename T, bool VEC, bool DIAG, int P>
+__device__ __forceinline__ void gram_task(const T *__restrict__ X, int64_t ld, int n, int rowA,
+                                          int rowB, int64_t k0, int64_t k1, d4v (&acc)[4][4]) {
+    const int lane = threadIdx.x & 63, rr = lane & 15, g = lane >> 4;
+    const T *pa[4];
+    const T *pb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int ra = min(rowA + i * 16 + rr, n - 1);
+        pa[i] = X + (int64_t)ra * ld + k0 + 2 * g;
+        const int rb = min(rowB + i * 16 + rr, n - 1);
+        pb[i] = X + (int64_t)rb * ld + k0 + 2 * g;
+    }
+    const int64_t len = k1 - k0;
+    const int64_t nb = len >> 3;
+    const int64_t rem = nb % P;
+
+    // (1) the first nb % P blocks, unpipelined, so the ring runs a multiple of P
+    for (int64_t kb = 0; kb < rem; ++kb) {
+        d2v a[4], b[4];
+        gram_load<T, VEC, DIAG>(pa, pb, kb * 8, a, b);
+        gram_mma<DIAG>(acc, a, b);
+    }
+    // (2) register ring, P k-blocks in flight
+    if (nb > rem) {
+        d2v ra[P][4], rb[P][4];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            gram_load<T, VEC, DIAG>(pa, pb, (rem + p) * 8, ra[p], rb[p]);
+            __builtin_amdgcn_sched_barrier(0);  // issue stages in ring order
+        }
+        for (int64_t kb = rem; kb < nb; kb += P) {
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                gram_mma<DIAG>(acc, ra[p], rb[p]);
+                int64_t nk = kb + P + p;
+                nk = nk < nb ? nk : nb - 1;  // clamped re-load past the end keeps waits static
+                gram_load<T, VEC, DIAG>(pa, pb, nk * 8, ra[p], rb[p]);
+                // keep the prefetch here: without the fence the scheduler sinks it to
+                // the top of the next trip and the ring degenerates to load-then-wait
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    // (3) ragged tail: len % 8 columns, guarded scalar loads
+    if (len & 7) {
+        const int64_t kt = nb * 8;
+        d2v a[4], b[4];
+        const bool v0 = kt + 2 * g < len, v1 = kt + 2 * g + 1 < len;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a[i].x = v0 ? (double)pa[i][kt] : 0.0;
+            a[i].y = v1 ? (double)pa[i][kt + 1] : 0.0;
+            b[i].x = v0 ? (double)pb[i][kt] : 0.0;
+            b[i].y = v1 ? (double)pb[i][kt + 1] : 0.0;
+        }
+        gram_mma<DIAG>(acc, a, b);
+    }
+}
+
+template <typename T, bool VEC, int P>
+__global__ __launch_bounds__(256, 1) void k_gram(const T *__restrict__ X, int64_t ld, int n,
+                                                 int64_t d, int T_, int ntile, int S, int64_t kc,
+                                                 int nwg, double *__restrict__ part) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lwg = xcd_remap(blockIdx.x, nwg);
+    const int task = lwg * 4 + wave;  // tasks are piece-major: task = s*ntile + u
+    if (task >= ntile * S) return;    // wave-uniform
+    const int s = task / ntile, u = task - s * ntile;
+    int bi, bj;
+    tri_decode(u, T_, bi, bj);
+    const int64_t k0 = (int64_t)s * kc;
+    const int64_t k1 = min(d, k0 + kc);
+
+    d4v acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = d4v{0.0, 0.0, 0.0, 0.0};
+
+    if (k1 > k0) {
+        if (bi == bj)
+            gram_task<T, VEC, true, P>(X, ld, n, bi * 64, bj * 64, k0, k1, acc);
+        else
+            gram_task<T, VEC, false, P>(X, ld, n, bi * 64, bj * 64, k0, k1, acc);
+    }
+
+    double *out = part + (int64_t)task * 4096;
+    const int rr = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = acc[i][j][r];
+}
+
+// ---------------------------------------------------------------------------
+// K1b: packed upper U[u][64][64] = sum_{s=0..S-1} part[s*ntile+u] (fixed order)
+// grid: ntile*16 blocks of 256 threads (4 rows x 64 cols each)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_reduce(const double *__restrict__ part, int ntile, int S,
+                                                double *__restrict__ U) {
+    const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
+    const int e = chunk * 256 + threadIdx.x;
+    const double *p = part + (int64_t)u * 4096 + e;
+    const int64_t stride = (int64_t)ntile * 4096;
+    double acc = 0.0;
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {
+        const double v0 = p[(s + 0) * stride], v1 = p[(s + 1) * stride];
+        const double v2 = p[(s + 2) * stride], v3 = p[(s + 3) * stride];
+        acc += v0;
+        acc += v1;
+        acc += v2;
+        acc += v3;
+    }
+    for (; s < S; ++s) acc += p[s * stride];
+    U[(int64_t)u * 4096 + e] = acc;
+}
+
+// Fixed-order sum of R packed partials (deterministic multi-GPU mode):
+// U[e] = sum_{r=0..R-1} Ug[r*stride + e]
+__global__ __launch_bounds__(256) void k_sum_ranks(const double *__restrict__ Ug, int R,
+                                                   int64_t stride, double *__restrict__ U) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= stride) return;
+    double acc = 0.0;
+    for (int r = 0; r < R; ++r) acc += Ug[(int64_t)r * stride + e];
+    U[e] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// K1c: packed upper -> symmetric G (n x n, row-major) + diag
+// grid: ntile*16 blocks; upper elements only (diagonal sub-tiles: i <= j)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_expand(const double *__restrict__ U, int n, int T_,
+                                                double *__restrict__ G, double *__restrict__ diag) {
+    const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
+    int bi, bj;
+    tri_decode(u, T_, bi, bj);
+    const int i = chunk * 4 + (threadIdx.x >> 6), j = threadIdx.x & 63;
+    const int r = bi * 64 + i, c = bj * 64 + j;
+    if (r >= n || c >= n) return;
+    if (bi == bj && j < i) return;
+    const double v = U[(int64_t)u * 4096 + i * 64 + j];
+    G[(int64_t)r * n + c] = v;
+    if (r != c)
+        G[(int64_t)c * n + r] = v;
+    else
+        diag[r] = v;
+}
+
+// ---------------------------------------------------------------------------
+// K2: score[i] = sum of ranks 1..k of sort(D[i])   (logistic_validator.py:62-63)
+// One workgroup per row; the row lives in LDS as order-preserving u64 keys.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void k_scores(const double *__restrict__ G,
+                                               const double *__restrict__ diag, int n, int npow2,
+                                               int64_t k, double *__restrict__ scores) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
+    __shared__ double red[NT / 64];
+    const int i = blockIdx.x, tid = threadIdx.x;
+    const double di = diag[i];
+    const double *Gi = G + (int64_t)i * n;
+    for (int j = tid; j < npow2; j += NT) {
+        uint64_t key = ~0ULL;  // padding sorts after every real value (NaN included)
+        if (j < n) {
+            const double t = di + diag[j];
+            const double g2 = 2.0 * Gi[j];
+            key = dkey(t - g2);
+        }
+        keys[j] = key;
+    }
+    __syncthreads();
+    for (int size = 2; size <= npow2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < (npow2 >> 1); t += NT) {
+                const int lo = 2 * t - (t & (stride - 1));
+                const int hi = lo + stride;
+                const bool asc = (lo & size) == 0;
+                const uint64_t a = keys[lo], b = keys[hi];
+                if ((a > b) == asc) {
+                    keys[lo] = b;
+                    keys[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    double acc = 0.0;
+    for (int64_t r = 1 + tid; r <= k; r += NT) acc += dkey_inv(keys[r]);
+    // fixed-shape reduction: wave butterfly, then waves in order
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((tid & 63) == 0) red[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) s += red[w];
+        scores[i] = (k > 0) ? s : 0.0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K3: rank_i = #{j : key_j < key_i} + #{j < i : key_j == key_i}; mask = rank < m
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rank(const double *__restrict__ scores, int n, int m,
+                                              int *__restrict__ mask) {
+    __shared__ uint64_t sk[2048];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const uint64_t ki = (i < n) ? dkey(scores[i]) : 0ULL;
+    int cnt = 0;
+    for (int base = 0; base < n; base += 2048) {
+        const int len = min(2048, n - base);
+        __syncthreads();
+        for (int j = threadIdx.x; j < len; j += 256) sk[j] = dkey(scores[base + j]);
+        __syncthreads();
+        for (int j = 0; j < len; ++j) {
+            const uint64_t kj = sk[j];
+            cnt += (kj < ki) || (kj == ki && base + j < i);
+        }
+    }
+    if (i < n) mask[i] = cnt < m ? 1 : 0;
+}
+
+// K3b: ascending compaction of mask (single workgroup of 1024 threads)
+__global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, int n,
+                                                  int64_t *__restrict__ sel) {
+    __shared__ int pre[1024];
+    const int tid = threadIdx.x;
+    const int chunk = (n + 1023) / 1024;
+    const int c0 = min(n, tid * chunk), c1 = min(n, c0 + chunk);
+    int cnt = 0;
+    for (int j = c0; j < c1; ++j) cnt += mask[j];
+    pre[tid] = cnt;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int v = tid >= o ? pre[tid - o] : 0;
+        __syncthreads();
+        pre[tid] += v;
+        __syncthreads();
+    }
+    int pos = pre[tid] - cnt;
+    for (int j = c0; j < c1; ++j)
+        if (mask[j]) sel[pos++] = j;
+}
+
+// ---------------------------------------------------------------------------
+// K4: mean[c] = (sum over selected rows, ascending) / m      (:51, fp64)
+// ---------------------------------------------------------------------------
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t ld, int64_t d,
+                                              const int64_t *__restrict__ sel, int m,
+                                              double *__restrict__ mean) {
+    extern __shared__ __attribute__((aligned(16))) int64_t srow[];  // row offsets (elements)
+    for (int r = threadIdx.x; r < m; r += 256) srow[r] = sel[r] * ld;
+    __syncthreads();
+    const double dm = (double)m;
+    const int64_t npair = (d + 1) >> 1;
+    for (int64_t cp = (int64_t)blockIdx.x * 256 + threadIdx.x; cp < npair;
+         cp += (int64_t)gridDim.x * 256) {
+        const int64_t c = cp * 2;
+        if (c + 1 < d) {
+            d2v acc = {0.0, 0.0};
+            int r = 0;
+            for (; r + 8 <= m; r += 8) {
+                d2v v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = ld2<T, VEC>(X + srow[r + q] + c);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    acc.x += v[q].x;
+                    acc.y += v[q].y;
+                }
+            }
+            for (; r < m; ++r) {
+                const d2v v = ld2<T, VEC>(X + srow[r] + c);
+                acc.x += v.x;
+                acc.y += v.y;
+            }
+            mean[c] = acc.x / dm;
+            mean[c + 1] = acc.y / dm;
+        } else {
+            double acc = 0.0;
+            for (int r = 0; r < m; ++r) acc += (double)X[srow[r] + c];
+            mean[c] = acc / dm;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic batch: grid (column blocks, rows)
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_synth(T *__restrict__ X, int64_t ld, int64_t dl,
+                                               int64_t c0, const int64_t *__restrict__ perm,
+                                               SynthParams P) {
+    const int64_t p = blockIdx.y;
+    const int64_t r = perm[p];
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < dl; k += (int64_t)gridDim.x * 256)
+        X[p * ld + k] = (T)synth_elem(P, r, c0 + k);
+}
+
+// ===========================================================================
+// launchers
+// ===========================================================================
+
+static constexpr int GRAM_P = 4;
+
+hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan &pl,
+                       double *part, hipStream_t st) {
+    const bool vec = dtype == 0 ? ((ld % 2) == 0 && ((uintptr_t)X % 16) == 0)
+                                : ((ld % 2) == 0 && ((uintptr_t)X % 8) == 0);
+    dim3 grid((unsigned)pl.nwg), block(256);
+    if (dtype == 0) {
+        if (vec)
+            hipLaunchKernelGGL((k_gram<double, true, GRAM_P>), grid, block, 0, st,
+                               (const double *)X, ld, n, d, pl.T, pl.ntile, pl.S, pl.kc, pl.nwg, part);
+        else
+            hipLaunchKernelGGL((k_gram<double, false, GRAM_P>), grid, block, 0, st,
+                               (const double *)X, ld, n, d, pl.T, pl.ntile, pl.S, pl.kc, pl.nwg, part);
+    } else {
+        if (vec)
+            hipLaunchKernelGGL((k_gram<float, true, GRAM_P>), grid, block, 0, st, (const float *)X,
+                               ld, n, d, pl.T, pl.ntile, pl.S, pl.kc, pl.nwg, part);
+        else
+            hipLaunchKernelGGL((k_gram<float, false, GRAM_P>), grid, block, 0, st, (const float *)X,
+                               ld, n, d, pl.T, pl.ntile, pl.S, pl.kc, pl.nwg, part);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce(const double *part, const Plan &pl, double *U, hipStream_t st) {
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)pl.ntile * 16), dim3(256), 0, st, part, pl.ntile,
+                       pl.S, U);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_ranks(const double *Ug, int R, int64_t stride, double *U, hipStream_t st) {
+    hipLaunchKernelGGL(k_sum_ranks, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, st, Ug, R,
+                       stride, U);
+    return hipGetLastError();
+}
+
+hipError_t launch_expand(const double *U, int n, int T, int ntile, double *G, double *diag,
+                         hipStream_t st) {
+    hipLaunchKernelGGL(k_expand, dim3((unsigned)ntile * 16), dim3(256), 0, st, U, n, T, G, diag);
+    return hipGetLastError();
+}
+
+static int next_pow2(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+hipError_t launch_scores(const double *G, const double *diag, int n, int64_t k, double *scores,
+                         hipStream_t st) {
+    const int np2 = next_pow2(n < 2 ? 2 : n);
+    const size_t lds = (size_t)np2 * sizeof(uint64_t);
+    if (np2 <= 2048) {
+        hipLaunchKernelGGL(k_scores<256>, dim3(n), dim3(256), lds, st, G, diag, n, np2, k, scores);
+    } else {
+        hipLaunchKernelGGL(k_scores<1024>, dim3(n), dim3(1024), lds, st, G, diag, n, np2, k, scores);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rank(const double *scores, int n, int m, int *mask, hipStream_t st) {
+    hipLaunchKernelGGL(k_rank, dim3((n + 255) / 256), dim3(256), 0, st, scores, n, m, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const int *mask, int n, int64_t *sel, hipStream_t st) {
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, st, mask, n, sel);
+    return hipGetLastError();
+}
+
+hipError_t launch_mean(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel, int m,
+                       double *mean, int num_cu, hipStream_t st) {
+    const int64_t npair = (d + 1) / 2;
+    int64_t blocks = (npair + 255) / 256;
+    const int64_t cap = (int64_t)num_cu * 16;
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    const size_t lds = (size_t)m * sizeof(int64_t);
+    const bool vec = dtype == 0 ? ((ld % 2) == 0 && ((uintptr_t)X % 16) == 0)
+                                : ((ld % 2) == 0 && ((uintptr_t)X % 8) == 0);
+    dim3 grid((unsigned)blocks), block(256);
+    if (dtype == 0) {
+        if (vec)
+            hipLaunchKernelGGL((k_mean<double, true>), grid, block, lds, st, (const double *)X, ld, d,
+                               sel, m, mean);
+        else
+            hipLaunchKernelGGL((k_mean<double, false>), grid, block, lds, st, (const double *)X, ld,
+                               d, sel, m, mean);
+    } else {
+        if (vec)
+            hipLaunchKernelGGL((k_mean<float, true>), grid, block, lds, st, (const float *)X, ld, d,
+                               sel, m, mean);
+        else
+            hipLaunchKernelGGL((k_mean<float, false>), grid, block, lds, st, (const float *)X, ld, d,
+                               sel, m, mean);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, int64_t c0,
+                        const int64_t *perm, const SynthParams &P, hipStream_t st) {
+    int64_t bx = (dl + 255) / 256;
+    if (bx > 4096) bx = 4096;
+    if (bx < 1) bx = 1;
+    dim3 grid((unsigned)bx, (unsigned)n), block(256);
+    if (dtype == 0)
+        hipLaunchKernelGGL(k_synth<double>, grid, block, 0, st, (double *)X, ld, dl, c0, perm, P);
+    else
+        hipLaunchKernelGGL(k_synth<float>, grid, block, 0, st, (float *)X, ld, dl, c0, perm, P);
+    return hipGetLastError();
+}
+
+hipError_t configure_kernels() {
+    // the row sort may need up to BK_MAX_N * 8 = 128 KiB of dynamic LDS
+    hipError_t e = hipFuncSetAttribute((const void *)k_scores<1024>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void *)k_scores<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            131072);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void *)k_mean<double, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void *)k_mean<double, false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void *)k_mean<float, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void *)k_mean<float, false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+}
+
+}  // namespace bk

@@ -1,0 +1,265 @@
+"""Host-side mirror of Biscotti's Multi-Krum verifier interface, on libbk.
+
+Reference surface kept (same names, argument meaning and error behaviour):
+
+  krum(deltas, clip)              ML/code/logistic_validator.py:36-49
+                                  (== ML/Pytorch/client_obj.py:114-127)
+  get_krum_scores(X, groupsize)   ML/code/logistic_validator.py:54-65
+  KRUMValidator                   DistSys/krum.go:22-29
+    .initialize()                 krum.go:31-44   (binds the engine instead of pyKRUMFunc)
+    .check_if_accepted(peer_id)   krum.go:47-73
+    .compute_scores()             krum.go:77-98
+    .get_top_krum_index(deltas)   krum.go:100-166 (the go-python call this engine replaces)
+    .flush_collected_updates()    krum.go:169-176
+  Update                          DistSys/update.go:13-22
+
+Differences a caller can observe, all documented in DESIGN.md:
+  * the selected indices come back ascending (a set; numpy returns
+    argpartition order, and the only consumer tests membership);
+  * ties at the selection boundary resolve to the lower index;
+  * clip = 0 raises ValueError, as np.argpartition does in the reference.
+
+Everything runs through libbk.so on the GPU; there is no CPU path.
+"""
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import ctypes
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+__all__ = ["Engine", "krum", "get_krum_scores", "krum_mean", "KRUMValidator", "Update",
+           "default_engine"]
+
+
+def _p(x):
+    return ctypes.c_void_p(x) if x is not None else None
+
+
+class Engine:
+    """One libbk context (bk_ctx) bound to one GPU."""
+
+    def __init__(self, device=0):
+        self._ctx = ctypes.c_void_p()
+        check(lib().bk_create(ctypes.byref(self._ctx), int(device)))
+        self.device = int(device)
+
+    def close(self):
+        if self._ctx:
+            lib().bk_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    # ---- host entry (bk_multikrum): numpy in, numpy out -----------------
+    def multikrum(self, X, f, want_scores=True, want_mean=True):
+        X = np.asarray(X)
+        if X.dtype not in (np.float64, np.float32):
+            X = X.astype(np.float64)
+        if X.ndim != 2:
+            raise ValueError("deltas must be 2-D (n updates x d)")
+        if X.strides[1] != X.itemsize or X.strides[0] % X.itemsize:
+            X = np.ascontiguousarray(X)
+        n, d = X.shape
+        ld = X.strides[0] // X.itemsize
+        f = int(f)
+        check(lib().bk_check_args(n, d, f))
+        m = n - f
+        sel = np.empty(m, dtype=np.int64)
+        mo = ctypes.c_int64(0)
+        sc = np.empty(n, dtype=np.float64) if want_scores else None
+        mean = np.empty(d, dtype=np.float64) if want_mean else None
+        dt = _lib.BK_F32 if X.dtype == np.float32 else _lib.BK_F64
+        check(lib().bk_multikrum(self._ctx, X.ctypes.data, _lib.BK_HOST, dt, n, d, ld, f,
+                                 sel.ctypes.data, ctypes.addressof(mo),
+                                 sc.ctypes.data if sc is not None else None,
+                                 mean.ctypes.data if mean is not None else None))
+        assert mo.value == m
+        return sel, sc, mean
+
+    # ---- device entry (bk_multikrum_device): raw device pointers --------
+    def multikrum_device_ptr(self, x_ptr, dtype, n, d, ld, f, sel_ptr, scores_ptr=None,
+                             mean_ptr=None):
+        check(lib().bk_multikrum_device(self._ctx, _p(x_ptr), dtype, n, d, ld, f, _p(sel_ptr),
+                                        _p(scores_ptr), _p(mean_ptr)))
+
+    def multikrum_sharded_ptr(self, x_ptr, dtype, n, d_local, ld, f, sel_ptr, scores_ptr=None,
+                              mean_ptr=None):
+        check(lib().bk_multikrum_sharded_device(self._ctx, _p(x_ptr), dtype, n, d_local, ld, f,
+                                                _p(sel_ptr), _p(scores_ptr), _p(mean_ptr)))
+
+    def gram_upper_ptr(self, x_ptr, dtype, n, d, ld, upper_ptr):
+        check(lib().bk_gram_upper_device(self._ctx, _p(x_ptr), dtype, n, d, ld, _p(upper_ptr)))
+
+    def finish_ptr(self, upper_ptr, x_ptr, dtype, n, d, ld, f, sel_ptr, scores_ptr=None,
+                   mean_ptr=None):
+        check(lib().bk_finish_device(self._ctx, _p(upper_ptr), _p(x_ptr), dtype, n, d, ld, f,
+                                     _p(sel_ptr), _p(scores_ptr), _p(mean_ptr)))
+
+    def synth_fill_ptr(self, x_ptr, dtype, n, d_local, ld, c0, d_total, seed, nbyz,
+                       mu_scale=0.01, byz_scale=0.05, sigma=1e-3, flags=0):
+        check(lib().bk_synth_fill_device(self._ctx, _p(x_ptr), dtype, n, d_local, ld, c0, d_total,
+                                         seed, nbyz, mu_scale, byz_scale, sigma, flags))
+
+    # ---- plumbing ------------------------------------------------------
+    def set_stream(self, stream_handle):
+        check(lib().bk_set_stream(self._ctx, _p(stream_handle)))
+
+    def stream(self):
+        return lib().bk_get_stream(self._ctx)
+
+    def synchronize(self):
+        check(lib().bk_synchronize(self._ctx))
+
+    def comm_init(self, nranks, rank, uid_bytes):
+        buf = ctypes.create_string_buffer(bytes(uid_bytes), _lib.BK_UNIQUE_ID_BYTES)
+        check(lib().bk_comm_init(self._ctx, int(nranks), int(rank), buf))
+
+    def comm_set_mode(self, deterministic):
+        check(lib().bk_comm_set_mode(self._ctx, 1 if deterministic else 0))
+
+    def timing_enable(self, on=True):
+        check(lib().bk_timing_enable(self._ctx, 1 if on else 0))
+
+    def timing_read(self):
+        out = {}
+        for i, name in enumerate(_lib.KERNELS):
+            ms = ctypes.c_double(0)
+            cnt = ctypes.c_int64(0)
+            check(lib().bk_timing_read(self._ctx, i, ctypes.byref(ms), ctypes.byref(cnt)))
+            if cnt.value:
+                out[name] = {"total_ms": ms.value, "count": cnt.value,
+                             "avg_ms": ms.value / cnt.value}
+        return out
+
+    def plan(self, n, d):
+        v = [ctypes.c_int64(0) for _ in range(4)]
+        check(lib().bk_plan(self._ctx, n, d, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("S", "kc", "ntile", "nwg"), (x.value for x in v)))
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(_lib.BK_UNIQUE_ID_BYTES)
+    check(lib().bk_comm_unique_id(buf))
+    return buf.raw
+
+
+_default = {}
+
+
+def default_engine(device=0):
+    if device not in _default:
+        _default[device] = Engine(device)
+    return _default[device]
+
+
+def _as_matrix(deltas):
+    # logistic_validator.py:41 -- deltas = np.array(deltas)
+    X = np.asarray(deltas)
+    if X.dtype not in (np.float64, np.float32):
+        X = np.array(deltas, dtype=np.float64)
+    return X
+
+
+def krum(deltas, clip, engine: Optional[Engine] = None):
+    """Indices of the n - clip updates with the lowest Krum scores.
+
+    Mirrors ``krum(deltas, clip)`` (logistic_validator.py:36-49); the result is
+    the same index set, returned ascending.
+    """
+    X = _as_matrix(deltas)
+    n = len(X)
+    if clip < 1 or clip >= n:
+        # np.argpartition(scores, n - clip) raises for kth == n (clip == 0)
+        raise ValueError("kth(=%d) out of bounds (%d)" % (n - clip, n))
+    sel, _, _ = (engine or default_engine()).multikrum(X, clip, want_scores=False,
+                                                       want_mean=False)
+    return sel
+
+
+def krum_mean(deltas, clip, engine: Optional[Engine] = None):
+    """(selected indices, mean of the selected deltas): the aggregate the
+    reference leaves commented out at logistic_validator.py:51."""
+    X = _as_matrix(deltas)
+    n = len(X)
+    if clip < 1 or clip >= n:
+        raise ValueError("kth(=%d) out of bounds (%d)" % (n - clip, n))
+    sel, _, mean = (engine or default_engine()).multikrum(X, clip, want_scores=False,
+                                                          want_mean=True)
+    return sel, mean
+
+
+def get_krum_scores(X, groupsize, engine: Optional[Engine] = None):
+    """Krum score of every row: sum of its groupsize-2 smallest distances to
+    the others (logistic_validator.py:54-65).  groupsize = n - clip."""
+    X = _as_matrix(X)
+    n = len(X)
+    f = n - int(groupsize)
+    if f < 1 or f >= n:
+        raise ValueError("groupsize must satisfy 1 <= n - groupsize < n")
+    _, sc, _ = (engine or default_engine()).multikrum(X, f, want_scores=True, want_mean=False)
+    return sc
+
+
+@dataclass
+class Update:
+    """DistSys/update.go:13-22 (the fields the verifier path reads)."""
+    SourceID: int
+    Iteration: int = 0
+    Delta: Optional[np.ndarray] = None
+    Commitment: bytes = b""
+    Noise: Optional[np.ndarray] = None
+    NoisedDelta: Optional[np.ndarray] = None
+    Accepted: bool = False
+    SignatureList: List[bytes] = field(default_factory=list)
+
+
+class KRUMValidator:
+    """DistSys/krum.go:22-29, with getTopKRUMIndex running on libbk."""
+
+    def __init__(self, num_adversaries=0.5, engine: Optional[Engine] = None, device=0):
+        self.UpdateList: List[Update] = []
+        self.AcceptedList: List[int] = []
+        self.NumAdversaries = num_adversaries  # fixed at 0.5 (main.go:783)
+        self._engine = engine
+        self._device = device
+
+    def initialize(self):
+        # krum.go:31-44 bound pyKRUMFunc; here: create the engine context
+        if self._engine is None:
+            self._engine = default_engine(self._device)
+        return self
+
+    def check_if_accepted(self, peer_id):
+        # krum.go:47-73 (the isPoisoning bypass at :51-58 is dead code: the
+        # global is never set, main.go:843 declares a local)
+        return any(self.UpdateList[i].SourceID == peer_id for i in self.AcceptedList)
+
+    def compute_scores(self):
+        # krum.go:77-98
+        running = [u.NoisedDelta for u in self.UpdateList]
+        self.AcceptedList = self.get_top_krum_index(running)
+
+    def get_top_krum_index(self, deltas) -> List[int]:
+        # krum.go:100-166: adversaryCount := int(NumAdversaries * float64(n))
+        n = len(deltas)
+        clip = int(self.NumAdversaries * float(n))
+        if self._engine is None:
+            self.initialize()
+        return [int(i) for i in krum(np.asarray(deltas, dtype=np.float64), clip, self._engine)]
+
+    def flush_collected_updates(self, collecting_updates=False):
+        # krum.go:169-176
+        if not collecting_updates:
+            self.UpdateList = []
+            self.AcceptedList = []

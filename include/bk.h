@@ -1,0 +1,157 @@
+/*
+ * bk.h -- C ABI of the MI355X-native Multi-Krum engine (libbk.so).
+ *
+ * Drop-in boundary for Biscotti's verifier hot path.  The reference path is
+ *
+ *   Peer.VerifyUpdateKRUM          DistSys/krum.go:227-365
+ *    -> KRUMValidator.computeScores  DistSys/krum.go:77-98
+ *     -> KRUMValidator.getTopKRUMIndex(deltas [][]float64) []int
+ *                                    DistSys/krum.go:100-166   <-- replaced
+ *        (go-python: marshal n*d PyFloats, call numpy krum(deltas, clip),
+ *         decode the int64 index bytes)
+ *         -> krum(deltas, clip)      ML/code/logistic_validator.py:36-49
+ *         -> get_krum_scores(X, g)   ML/code/logistic_validator.py:54-65
+ *         (aggregate: np.mean(deltas[good_idx], 0), logistic_validator.py:51)
+ *
+ * A cgo shim with the same Go signature as getTopKRUMIndex calls bk_multikrum
+ * (see INTEGRATION.md).  Plain pointers and sizes only; no torch, no HIP types.
+ *
+ * Conventions
+ *   X        row-major n x d with leading dimension ld (elements), fp64 or fp32
+ *            (fp32 is widened exactly; every accumulation is fp64).
+ *   f        number of updates to reject ("clip"; krum.go:110 computes
+ *            int(0.5*n)).  Valid iff 1 <= f < n (f = 0 makes the reference's
+ *            np.argpartition raise ValueError, logistic_validator.py:45).
+ *   m = n-f  number selected; k = max(0, n-f-2) neighbours summed per score.
+ *   sel_idx  the m selected row indices, ASCENDING (a set: the only consumer,
+ *            checkIfAccepted krum.go:47-73, tests membership).  Ties at the
+ *            selection boundary resolve to the lower index; NaN scores order
+ *            last (as numpy's sort/argpartition do).
+ *   mean     (1/m) * sum of selected rows (fp64), the north-star aggregate.
+ *
+ * Errors: every entry returns 0 (BK_OK) or a negative bk_status; the message
+ * is in bk_last_error() (thread-local).  Nothing aborts or throws across the
+ * ABI.  Calls on one context are serialised internally; each entry selects the
+ * context's device itself (goroutines migrate between OS threads).
+ */
+#ifndef BK_H_
+#define BK_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BK_ABI_VERSION 1
+
+typedef struct bk_ctx bk_ctx;
+
+enum bk_status {
+    BK_OK = 0,
+    BK_EINVAL = -1,  /* bad n, d, f, ld, dtype, pointer or mode             */
+    BK_ENOMEM = -2,  /* device / pinned allocation failed                    */
+    BK_EHIP = -3,    /* a HIP runtime call failed                            */
+    BK_ERCCL = -4,   /* an RCCL call failed / communicator missing          */
+    BK_ENOTSUP = -5  /* shape outside what this build supports (n > BK_MAX_N) */
+};
+
+enum bk_dtype { BK_F64 = 0, BK_F32 = 1 };
+enum bk_where { BK_HOST = 0, BK_HOST_PINNED = 1, BK_DEVICE = 2 };
+
+#define BK_MAX_N 16384
+
+/* ---- library ------------------------------------------------------------ */
+int bk_abi_version(void);
+const char *bk_last_error(void);
+/* Argument check only (no GPU needed): BK_OK or BK_EINVAL / BK_ENOTSUP. */
+int bk_check_args(int64_t n, int64_t d, int64_t f);
+
+/* ---- context: replaces KRUMValidator.initialize() (krum.go:31-44), which
+ *      bound pyKRUMFunc from the module imported in pyInit (honest.go:204-258) */
+int bk_create(bk_ctx **out, int device);
+void bk_destroy(bk_ctx *ctx);
+/* Run on a caller stream (hipStream_t passed as void*); NULL = own stream. */
+int bk_set_stream(bk_ctx *ctx, void *hip_stream);
+void *bk_get_stream(bk_ctx *ctx);
+int bk_synchronize(bk_ctx *ctx);
+/* C-owned pinned staging for callers that must copy (cgo: Go pointers may not
+ * be retained by C, so the shim packs [][]float64 rows here). */
+int bk_stage_alloc(bk_ctx *ctx, int64_t bytes, void **pinned);
+int bk_stage_free(bk_ctx *ctx, void *pinned);
+
+/* ---- the drop-in: getTopKRUMIndex (krum.go:100-166) + numpy krum ---------
+ * X on host (BK_HOST / BK_HOST_PINNED: copied H2D) or device (BK_DEVICE).
+ * Outputs are HOST pointers: sel_idx (m entries), m_out, scores (n, nullable),
+ * mean_out (d, nullable).  Synchronous. */
+int bk_multikrum(bk_ctx *ctx, const void *X, int where, int dtype, int64_t n, int64_t d,
+                 int64_t ld, int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
+                 double *mean_out);
+
+/* Device-resident, asynchronous on the context stream.  All pointers are
+ * device pointers; d_sel_idx gets m = n-f ascending indices; d_scores (n) and
+ * d_mean (d) are nullable. */
+int bk_multikrum_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
+                        int64_t ld, int64_t f, int64_t *d_sel_idx, double *d_scores,
+                        double *d_mean);
+
+/* ---- dimension-sharded stages (one process / device per column shard) ----
+ * Packed upper-triangle Gram: bk_upper_elems(n) doubles.  Summing the packed
+ * partials of all shards gives the Gram of the full batch. */
+int64_t bk_upper_elems(int64_t n);
+int bk_gram_upper_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
+                         int64_t ld, double *d_upper);
+/* Scores + selection from a (summed) packed Gram, then the mean of this
+ * shard's d columns of dX (d_mean nullable). */
+int bk_finish_device(bk_ctx *ctx, const double *d_upper, const void *dX, int dtype, int64_t n,
+                     int64_t d, int64_t ld, int64_t f, int64_t *d_sel_idx, double *d_scores,
+                     double *d_mean);
+
+/* ---- RCCL (one rank per process, xGMI) ------------------------------------ */
+#define BK_UNIQUE_ID_BYTES 128
+int bk_comm_unique_id(void *id_out /* BK_UNIQUE_ID_BYTES */);
+int bk_comm_init(bk_ctx *ctx, int nranks, int rank, const void *id /* BK_UNIQUE_ID_BYTES */);
+/* 0: ncclAllReduce(sum) of the packed Gram (default);
+ * 1: deterministic -- ncclAllGather of the partials + fixed rank-order sum. */
+int bk_comm_set_mode(bk_ctx *ctx, int deterministic);
+/* Partial Gram of the local column shard -> all-reduce -> scores/selection
+ * (redundant on every rank) -> mean of the local columns.  Async on stream. */
+int bk_multikrum_sharded_device(bk_ctx *ctx, const void *dX_local, int dtype, int64_t n,
+                                int64_t d_local, int64_t ld, int64_t f, int64_t *d_sel_idx,
+                                double *d_scores, double *d_mean_local);
+
+/* ---- synthetic batches (spec: DESIGN.md "Synthetic inputs") --------------
+ * Rows [0,n) x columns [c0, c0+d_local) of the n x d_total batch, generated on
+ * the device bit-identically to oracle/krum_oracle.c and the numpy spec. */
+#define BK_SYNTH_FP32ROUND 1
+int bk_synth_fill_device(bk_ctx *ctx, void *dX, int dtype, int64_t n, int64_t d_local,
+                         int64_t ld, int64_t c0, int64_t d_total, uint64_t seed, int64_t nbyz,
+                         double mu_scale, double byz_scale, double sigma, int flags);
+
+/* ---- measurement: per-kernel HIP-event timing on the context stream ------- */
+enum bk_kernel_id {
+    BK_K_GRAM = 0,     /* K1  fp64-MFMA split-K upper-triangle Gram partials */
+    BK_K_REDUCE = 1,   /* K1b fixed-order split-K reduce -> packed upper     */
+    BK_K_EXPAND = 2,   /* K1c packed upper -> symmetric G + diag            */
+    BK_K_SCORES = 3,   /* K2  distance row, bitonic sort, sum ranks 1..k    */
+    BK_K_RANK = 4,     /* K3  selection rank + mask                          */
+    BK_K_COMPACT = 5,  /* K3b mask -> ascending sel_idx                      */
+    BK_K_MEAN = 6,     /* K4  masked mean of the selected rows               */
+    BK_K_ALLREDUCE = 7,/* C1  RCCL exchange of the packed Gram               */
+    BK_K_SYNTH = 8,
+    BK_K_H2D = 9,
+    BK_K_D2H = 10,
+    BK_NUM_KERNELS = 11
+};
+int bk_timing_enable(bk_ctx *ctx, int on);   /* clears accumulated timings */
+int bk_timing_read(bk_ctx *ctx, int kernel_id, double *total_ms, int64_t *count);
+const char *bk_kernel_name(int kernel_id);
+/* The split-K plan K1 uses for a shape: pieces S, piece length kc (columns),
+ * 64x64 upper sub-tiles ntile, workgroups nwg. */
+int bk_plan(bk_ctx *ctx, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *ntile,
+            int64_t *nwg);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BK_H_ */

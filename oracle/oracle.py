@@ -1,0 +1,155 @@
+"""ctypes wrapper for the CPU oracle (oracle/libkrum_oracle.so).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by biscotti_amd/.  See krum_oracle.c for the
+reference file:line each function restates.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libkrum_oracle.so")
+_lib = None
+
+_i64 = ctypes.c_int64
+_vp = ctypes.c_void_p
+
+
+def build():
+    """Compile the oracle with its Makefile (gcc; no GPU needed)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_check_args.argtypes = [_i64, _i64, _i64]
+        L.oracle_check_args.restype = ctypes.c_int
+        L.oracle_krum.argtypes = [_vp, ctypes.c_int, _i64, _i64, _i64, _i64, _vp, _vp, _vp]
+        L.oracle_krum.restype = _i64
+        L.oracle_krum_scores.argtypes = [_vp, ctypes.c_int, _i64, _i64, _i64, _i64, _vp, _vp]
+        L.oracle_krum_scores.restype = ctypes.c_int
+        L.oracle_gram.argtypes = [_vp, ctypes.c_int, _i64, _i64, _i64, _vp]
+        L.oracle_gram.restype = ctypes.c_int
+        L.oracle_sqnorms.argtypes = [_vp, ctypes.c_int, _i64, _i64, _i64, _vp]
+        L.oracle_sqnorms.restype = ctypes.c_int
+        L.oracle_select.argtypes = [_vp, _i64, _i64, _vp]
+        L.oracle_select.restype = _i64
+        L.oracle_mean.argtypes = [_vp, ctypes.c_int, _i64, _i64, _vp, _i64, _vp]
+        L.oracle_mean.restype = None
+        L.oracle_synth_fill.argtypes = [_vp, ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
+                                        ctypes.c_uint64, _i64, ctypes.c_double, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_int]
+        L.oracle_synth_fill.restype = None
+        L.oracle_synth_perm.argtypes = [ctypes.c_uint64, _i64, _vp]
+        L.oracle_synth_perm.restype = None
+        L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_set_threads.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _x(X):
+    X = np.asarray(X)
+    if X.dtype not in (np.float64, np.float32):
+        X = X.astype(np.float64)
+    if X.ndim != 2 or X.strides[1] != X.itemsize:
+        X = np.ascontiguousarray(X)
+    ld = X.strides[0] // X.itemsize
+    return X, int(X.dtype == np.float32), ld
+
+
+def krum(X, f, want_scores=True, want_mean=True):
+    """Returns (sel ascending int64[m], scores float64[n] | None, mean float64[d] | None)."""
+    X, is32, ld = _x(X)
+    n, d = X.shape
+    if lib().oracle_check_args(n, d, f) != 0:
+        raise ValueError("invalid Multi-Krum arguments n=%d d=%d f=%d" % (n, d, f))
+    m = n - f
+    sel = np.empty(m, dtype=np.int64)
+    sc = np.empty(n, dtype=np.float64) if want_scores else None
+    mean = np.empty(d, dtype=np.float64) if want_mean else None
+    r = lib().oracle_krum(_ptr(X), is32, n, d, ld, f, _ptr(sel), _ptr(sc), _ptr(mean))
+    if r < 0:
+        raise RuntimeError("oracle_krum failed: %d" % r)
+    return sel, sc, mean
+
+
+def krum_scores(X, groupsize, want_D=False):
+    X, is32, ld = _x(X)
+    n, d = X.shape
+    sc = np.empty(n, dtype=np.float64)
+    D = np.empty((n, n), dtype=np.float64) if want_D else None
+    r = lib().oracle_krum_scores(_ptr(X), is32, n, d, ld, groupsize, _ptr(sc), _ptr(D))
+    if r:
+        raise RuntimeError("oracle_krum_scores failed: %d" % r)
+    return (sc, D) if want_D else sc
+
+
+def gram(X):
+    X, is32, ld = _x(X)
+    n, d = X.shape
+    G = np.empty((n, n), dtype=np.float64)
+    lib().oracle_gram(_ptr(X), is32, n, d, ld, _ptr(G))
+    return G
+
+
+def sqnorms(X):
+    X, is32, ld = _x(X)
+    n, d = X.shape
+    sq = np.empty(n, dtype=np.float64)
+    lib().oracle_sqnorms(_ptr(X), is32, n, d, ld, _ptr(sq))
+    return sq
+
+
+def select(scores, m):
+    scores = np.ascontiguousarray(scores, dtype=np.float64)
+    sel = np.empty(m, dtype=np.int64)
+    lib().oracle_select(_ptr(scores), len(scores), m, _ptr(sel))
+    return sel
+
+
+def mean(X, sel):
+    X, is32, ld = _x(X)
+    n, d = X.shape
+    sel = np.ascontiguousarray(sel, dtype=np.int64)
+    out = np.empty(d, dtype=np.float64)
+    lib().oracle_mean(_ptr(X), is32, d, ld, _ptr(sel), len(sel), _ptr(out))
+    return out
+
+
+def synth(n, d, seed, nbyz, mu_scale=0.01, byz_scale=0.05, sigma=1e-3, flags=0,
+          dtype=np.float64, c0=0, dl=None, d_total=None):
+    if dl is None:
+        dl = d - c0
+    if d_total is None:
+        d_total = d
+    X = np.empty((n, dl), dtype=dtype)
+    lib().oracle_synth_fill(_ptr(X), int(X.dtype == np.float32), n, dl, dl, c0, d_total,
+                            seed, nbyz, mu_scale, byz_scale, sigma, flags)
+    return X
+
+
+def synth_perm(seed, n):
+    p = np.empty(n, dtype=np.int64)
+    lib().oracle_synth_perm(seed, n, _ptr(p))
+    return p
+
+
+def set_threads(t):
+    lib().oracle_set_threads(int(t))
+
+
+def num_threads():
+    return lib().oracle_num_threads()

@@ -1,0 +1,97 @@
+"""libbk.so: loads, exports every symbol include/bk.h declares, validates
+arguments without a GPU, and fails loudly (an error status, never a CPU
+fallback) when no GPU is present."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from biscotti_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(REPO, "include", "bk.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(bk_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("bk_create", "bk_destroy", "bk_multikrum", "bk_multikrum_device",
+                 "bk_last_error", "bk_multikrum_sharded_device", "bk_comm_init"):
+        assert must in names
+    assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"amdgcn-amd-amdhsa" in data
+
+
+def test_abi_version_and_names():
+    L = _lib.lib()
+    assert L.bk_abi_version() == 1
+    assert L.bk_kernel_name(0) == b"k_gram"
+    assert L.bk_kernel_name(99) == b"?"
+    assert len(_lib.KERNELS) == 11
+
+
+@pytest.mark.parametrize("n,d,f,status", [
+    (10, 25, 2, 0), (10, 25, 0, -1), (10, 25, 10, -1), (10, 25, -1, -1), (0, 25, 1, -1),
+    (10, 0, 2, -1), (2, 1, 1, 0), (16385, 8, 3, -5), (16384, 8, 3, 0)])
+def test_check_args(n, d, f, status):
+    assert _lib.lib().bk_check_args(n, d, f) == status
+    if status:
+        assert _lib.last_error()
+
+
+def test_upper_elems():
+    L = _lib.lib()
+    assert L.bk_upper_elems(1) == 4096
+    assert L.bk_upper_elems(64) == 4096
+    assert L.bk_upper_elems(65) == 3 * 4096
+    assert L.bk_upper_elems(512) == 36 * 4096
+
+
+def test_plan_fills_the_chip():
+    L = _lib.lib()
+    v = [ctypes.c_int64() for _ in range(4)]
+    assert L.bk_plan(None, 512, 1 << 20, *[ctypes.byref(x) for x in v]) == 0
+    S, kc, ntile, nwg = (x.value for x in v)
+    assert ntile == 36 and kc % 8 == 0 and S * kc >= 1 << 20 and (S - 1) * kc < 1 << 20
+    tasks = ntile * S
+    waves = 256 * 4
+    assert tasks % waves == 0 or tasks % waves >= 0.9 * waves  # >= 90% of the last round busy
+    assert nwg == (tasks + 3) // 4
+
+
+def test_null_and_bad_arguments_do_not_crash():
+    L = _lib.lib()
+    assert L.bk_create(None, 0) == _lib.BK_EINVAL
+    assert L.bk_multikrum(None, None, 0, 0, 10, 10, 10, 2, None, None, None, None) == _lib.BK_EINVAL
+    assert L.bk_set_stream(None, None) == _lib.BK_EINVAL
+    assert L.bk_timing_read(None, 0, None, None) == _lib.BK_EINVAL
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    ctx = ctypes.c_void_p()
+    st = _lib.lib().bk_create(ctypes.byref(ctx), 0)
+    assert st in (_lib.BK_EHIP, _lib.BK_EINVAL)
+    assert _lib.last_error()
+    from biscotti_amd.krum import Engine
+    with pytest.raises((RuntimeError, ValueError)):
+        Engine(0)

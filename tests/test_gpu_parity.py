@@ -1,0 +1,202 @@
+"""Parity of the HIP path (libbk.so, through its C ABI) on an MI355X.
+
+* every small golden (produced by the reference numpy krum, see
+  tests/golden/gen_goldens.py): selected set bit-exact, scores within 1e-9 of
+  the max score, mean within 1e-9 of the norm-wise scale;
+* the BASELINE.json configs at full size (C, D f=153 / f=256, E fp32) against
+  their goldens, with the batch generated on the device;
+* the CPU oracle on shapes and layouts the goldens do not cover (ld padding,
+  misaligned base, fp32, n not a multiple of 64, tiny/huge k);
+* the sharded decomposition (partial Grams summed) == the unsharded call;
+* run-to-run bitwise determinism; argument errors; the GPU generator == CPU.
+"""
+import numpy as np
+import pytest
+
+import golden_util as GU
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from biscotti_amd import _lib  # noqa: E402
+
+
+def _dev_run(engine, Xt, f, dtype=None):
+    n, d = Xt.shape
+    dt = _lib.BK_F32 if Xt.dtype == torch.float32 else _lib.BK_F64
+    sel = torch.empty(n - f, dtype=torch.int64, device=Xt.device)
+    sc = torch.empty(n, dtype=torch.float64, device=Xt.device)
+    mean = torch.empty(d, dtype=torch.float64, device=Xt.device)
+    engine.multikrum_device_ptr(Xt.data_ptr(), dt, n, d, Xt.stride(0), f, sel.data_ptr(),
+                                sc.data_ptr(), mean.data_ptr())
+    engine.synchronize()
+    return sel.cpu().numpy(), sc.cpu().numpy(), mean.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", GU.small_cases())
+def test_small_goldens(name, engine, oracle):
+    X, p = GU.build_input(name, oracle)
+    rec = GU.manifest()[name]
+    if p["error"]:
+        with pytest.raises(ValueError):
+            engine.multikrum(X, p["f"])
+        return
+    g = GU.load(name)
+    sel, sc, mean = engine.multikrum(X, p["f"])
+    assert np.array_equal(sel, g["sel"]), (name, sel, g["sel"])
+    GU.check_scores(sc, g, rel=1e-9)
+    GU.check_mean(mean, g, rec)
+
+
+@pytest.mark.parametrize("name", GU.large_cases())
+def test_large_goldens_device_resident(name, engine):
+    p = GU.C.case_params(name)
+    n, d, f = p["n"], p["d"], p["f"]
+    tdt = torch.float32 if p["dtype"] == "float32" else torch.float64
+    dt = _lib.BK_F32 if p["dtype"] == "float32" else _lib.BK_F64
+    X = torch.empty((n, d), dtype=tdt, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), dt, n, d, X.stride(0), 0, d, p["seed"], p["nbyz"],
+                          p["mu_scale"], p["byz_scale"], p["sigma"], p["flags"])
+    sel, sc, mean = _dev_run(engine, X, f)
+    g = GU.load(name)
+    assert np.array_equal(sel, g["sel"])
+    GU.check_scores(sc, g, rel=1e-9)
+    GU.check_mean(mean, g, GU.manifest()[name])
+    # size-independent properties: m distinct ascending indices; every
+    # selected score <= every rejected score
+    assert len(np.unique(sel)) == n - f and np.all(np.diff(sel) > 0)
+    rej = np.setdiff1d(np.arange(n), sel)
+    assert np.max(sc[sel]) <= np.min(sc[rej])
+    del X
+    torch.cuda.empty_cache()
+
+
+def test_gpu_generator_matches_cpu(engine, oracle):
+    for (n, d, nbyz, flags, tdt, dt) in [(37, 1003, 5, 0, torch.float64, _lib.BK_F64),
+                                         (100, 785, 30, 1, torch.float64, _lib.BK_F64),
+                                         (64, 300, 20, 0, torch.float32, _lib.BK_F32)]:
+        X = torch.empty((n, d + 3), dtype=tdt, device="cuda")  # padded ld
+        engine.synth_fill_ptr(X.data_ptr(), dt, n, d, X.stride(0), 0, d, 77, nbyz, flags=flags)
+        engine.synchronize()
+        ref = oracle.synth(n, d, 77, nbyz, flags=flags,
+                           dtype=np.float32 if tdt == torch.float32 else np.float64)
+        got = X[:, :d].cpu().numpy()
+        assert np.array_equal(got.view(np.uint8), ref.view(np.uint8))
+        # a column shard of the same batch
+        Xs = torch.empty((n, 100), dtype=tdt, device="cuda")
+        engine.synth_fill_ptr(Xs.data_ptr(), dt, n, 100, 100, 200, d, 77, nbyz, flags=flags)
+        engine.synchronize()
+        assert np.array_equal(Xs.cpu().numpy().view(np.uint8),
+                              np.ascontiguousarray(ref[:, 200:300]).view(np.uint8))
+
+
+@pytest.mark.parametrize("n,d,f,pad,dtype", [
+    (1, 8, 0, 0, np.float64),      # n=1 -> invalid
+    (2, 1, 1, 0, np.float64), (3, 7, 1, 1, np.float64), (64, 64, 20, 0, np.float64),
+    (65, 129, 30, 2, np.float64), (128, 1000, 1, 0, np.float64), (200, 333, 198, 0, np.float64),
+    (257, 2049, 77, 5, np.float32), (300, 40000, 90, 0, np.float32), (513, 4099, 153, 0, np.float64),
+    (40, 100003, 12, 0, np.float64)])
+def test_against_oracle(engine, oracle, n, d, f, pad, dtype):
+    X = oracle.synth(n, d, 1000 + n + d, max(0, min(f, n)), dtype=dtype)
+    if pad:
+        Xp = np.zeros((n, d + pad), dtype=dtype)
+        Xp[:, :d] = X
+        Xv = Xp[:, :d]  # ld = d + pad (odd pads exercise the unaligned kernel variants)
+    else:
+        Xv = X
+    if f < 1 or f >= n:
+        with pytest.raises(ValueError):
+            engine.multikrum(Xv, f)
+        return
+    sel, sc, mean = engine.multikrum(Xv, f)
+    osel, osc, omean = oracle.krum(X, f)
+    assert np.array_equal(sel, osel)
+    scale = max(1e-300, np.max(np.abs(osc)))
+    assert np.max(np.abs(sc - osc)) <= 1e-9 * scale
+    mscale = np.max(np.mean(np.abs(X[osel].astype(np.float64)), axis=0))
+    assert np.max(np.abs(mean - omean)) <= 1e-9 * mscale
+
+
+def test_misaligned_device_pointer(engine, oracle):
+    n, d, f = 70, 999, 20
+    X = oracle.synth(n, d, 5, 20)
+    buf = torch.zeros(n * d + 1, dtype=torch.float64, device="cuda")
+    view = buf[1:].view(n, d)  # 8-B aligned, not 16-B: scalar-load kernels
+    view.copy_(torch.from_numpy(X).cuda())
+    sel, sc, mean = _dev_run(engine, view, f)
+    osel, osc, omean = oracle.krum(X, f)
+    assert np.array_equal(sel, osel)
+    assert np.max(np.abs(mean - omean)) <= 1e-9 * np.max(np.abs(omean)) * 10
+
+
+def test_deterministic_bitwise(engine):
+    n, d, f = 512, 200003, 153
+    X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 42, 153)
+    a = _dev_run(engine, X, f)
+    b = _dev_run(engine, X, f)
+    for u, v in zip(a, b):
+        assert np.array_equal(u.view(np.uint8), v.view(np.uint8))
+
+
+def test_sharded_decomposition_equals_full(engine):
+    """Packed partial Grams of column shards, summed, then finished == one
+    unsharded call: the multi-GPU path's math on the real kernels."""
+    from biscotti_amd.dist import all_shards
+    n, d, f = 300, 50000, 90
+    X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 9, 90)
+    usz = int(_lib.lib().bk_upper_elems(n))
+    acc = torch.zeros(usz, dtype=torch.float64, device="cuda")
+    for c0, dl in all_shards(d, 4):
+        U = torch.empty(usz, dtype=torch.float64, device="cuda")
+        Xs = X[:, c0:c0 + dl]
+        engine.gram_upper_ptr(Xs.data_ptr(), _lib.BK_F64, n, dl, X.stride(0), U.data_ptr())
+        engine.synchronize()
+        acc += U
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    sc = torch.empty(n, dtype=torch.float64, device="cuda")
+    mean = torch.empty(d, dtype=torch.float64, device="cuda")
+    engine.finish_ptr(acc.data_ptr(), X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr(),
+                      sc.data_ptr(), mean.data_ptr())
+    engine.synchronize()
+    fsel, fsc, fmean = _dev_run(engine, X, f)
+    assert np.array_equal(sel.cpu().numpy(), fsel)
+    s = sc.cpu().numpy()
+    assert np.max(np.abs(s - fsc)) <= 1e-12 * np.max(np.abs(fsc))
+    assert np.array_equal(mean.cpu().numpy(), fmean)
+    # single-rank sharded entry (no communicator needed) == unsharded
+    sel2 = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    engine.multikrum_sharded_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel2.data_ptr())
+    engine.synchronize()
+    assert np.array_equal(sel2.cpu().numpy(), fsel)
+
+
+def test_validator_end_to_end(engine, oracle):
+    from biscotti_amd.krum import KRUMValidator, Update, get_krum_scores, krum, krum_mean
+    X = oracle.synth(10, 25, 20261016, 2)
+    v = KRUMValidator(engine=engine).initialize()
+    v.UpdateList = [Update(SourceID=100 + i, NoisedDelta=X[i]) for i in range(10)]
+    v.compute_scores()
+    osel, osc, omean = oracle.krum(X, 5)  # clip = int(0.5 * 10)
+    assert v.AcceptedList == osel.tolist()
+    for i in range(10):
+        assert v.check_if_accepted(100 + i) == (i in osel)
+    assert np.array_equal(krum(X.tolist(), 2, engine), oracle.krum(X, 2)[0])
+    sc = get_krum_scores(X, 8, engine)
+    assert np.max(np.abs(sc - oracle.krum(X, 2)[1])) <= 1e-9 * np.max(np.abs(sc))
+    s, m = krum_mean(X, 2, engine)
+    assert np.array_equal(s, oracle.krum(X, 2)[0])
+
+
+def test_timing_api(engine):
+    n, d, f = 128, 4096, 30
+    X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 1, 30)
+    engine.timing_enable(True)
+    for _ in range(3):
+        _dev_run(engine, X, f)
+    t = engine.timing_read()
+    engine.timing_enable(False)
+    for k in ("k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean"):
+        assert t[k]["count"] == 3 and t[k]["avg_ms"] > 0
