@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <new>
 #include <string>
@@ -85,6 +86,14 @@ struct bk_ctx {
     std::vector<hipEvent_t> pool;
     double tot_ms[BK_NUM_KERNELS] = {0};
     int64_t cnt[BK_NUM_KERNELS] = {0};
+    // K1 v3 plans (device tables), cached per (n, d)
+    struct CachedPlan {
+        int n;
+        int64_t d;
+        Plan3 p;
+    };
+    std::vector<CachedPlan> plans;
+    int gram_variant = 3;  // 3: LDS-shared v3 for aligned fp64; 1: v1 everywhere (BK_GRAM=v1)
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -185,9 +194,77 @@ int check_common(bk_ctx *c, const void *X, int dtype, int64_t n, int64_t d, int6
 
 size_t esize(int dtype) { return dtype == BK_F64 ? 8 : 4; }
 
+void free_plan(Plan3 &p) {
+    if (p.d_groups) (void)hipFree(p.d_groups);
+    if (p.d_wg) (void)hipFree(p.d_wg);
+    if (p.d_red) (void)hipFree(p.d_red);
+    p.d_groups = nullptr;
+    p.d_wg = p.d_red = nullptr;
+}
+
+int get_plan3(bk_ctx *c, int64_t n, int64_t d, Plan3 **out) {
+    for (auto &cp : c->plans)
+        if (cp.n == n && cp.d == d) {
+            *out = &cp.p;
+            return BK_OK;
+        }
+    Plan3Host H = build_plan3((int)n, d, c->num_cu);
+    for (int u = 0; u < H.ntile; ++u)
+        if (H.red[3 * u + 1] < 0) return fail(BK_EHIP, "internal: K1 plan misses sub-tile %d", u);
+    Plan3 p;
+    p.n = (int)n;
+    p.d = d;
+    p.T = H.T;
+    p.ntile = H.ntile;
+    p.ngroups = (int)H.groups.size();
+    p.nwg = (int)H.wg.size() / 2;
+    p.nfull = H.nfull;
+    hipError_t e = hipMalloc(&p.d_groups, H.groups.size() * sizeof(GroupDesc));
+    if (e == hipSuccess) e = hipMalloc(&p.d_wg, H.wg.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&p.d_red, H.red.size() * sizeof(int));
+    if (e == hipSuccess)
+        e = hipMemcpy(p.d_groups, H.groups.data(), H.groups.size() * sizeof(GroupDesc),
+                      hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(p.d_wg, H.wg.data(), H.wg.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(p.d_red, H.red.data(), H.red.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        free_plan(p);
+        return fail(BK_ENOMEM, "K1 plan tables: %s", hipGetErrorString(e));
+    }
+    if (c->plans.size() >= 8) {
+        free_plan(c->plans.front().p);
+        c->plans.erase(c->plans.begin());
+    }
+    c->plans.push_back({(int)n, d, p});
+    *out = &c->plans.back().p;
+    return BK_OK;
+}
+
+bool use_v3(bk_ctx *c, const void *dX, int dtype, int64_t ld) {
+    return c->gram_variant == 3 && dtype == BK_F64 && (ld % 2) == 0 && ((uintptr_t)dX % 16) == 0;
+}
+
 // K1 + K1b: packed upper-triangle Gram of this call's columns into U
 int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
                double *U, Plan &pl) {
+    if (use_v3(c, dX, dtype, ld)) {
+        Plan3 *p3 = nullptr;
+        CHK(get_plan3(c, n, d, &p3));
+        pl.n = (int)n;
+        pl.d = d;
+        pl.T = p3->T;
+        pl.ntile = p3->ntile;
+        CHK(ensure(c->part, (size_t)p3->nwg * 16 * 4096 * sizeof(double)));
+        double *part = (double *)c->part.p;
+        const Plan3 &P3 = *p3;
+        CHK(timed(c, BK_K_GRAM, [&] {
+            return launch_gram3((const double *)dX, ld, (int)n, d, P3, part, c->stream);
+        }));
+        CHK(timed(c, BK_K_REDUCE, [&] { return launch_reduce3(part, P3, U, c->stream); }));
+        return BK_OK;
+    }
     pl = make_plan(n, d, c->num_cu, (size_t)n * d * esize(dtype));
     CHK(ensure(c->part, (size_t)pl.ntile * pl.S * 4096 * sizeof(double)));
     double *part = (double *)c->part.p;
@@ -293,6 +370,8 @@ int bk_create(bk_ctx **out, int device) {
         return fail(BK_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     c->stream = c->own;
+    if (const char *v = getenv("BK_GRAM"))
+        if (strcmp(v, "v1") == 0) c->gram_variant = 1;
     e = configure_kernels();
     if (e != hipSuccess) {
         (void)hipStreamDestroy(c->own);
@@ -319,6 +398,7 @@ void bk_destroy(bk_ctx *c) {
             (void)hipEventDestroy(ev.b);
         }
         for (hipEvent_t ev : c->pool) (void)hipEventDestroy(ev);
+        for (auto &cp : c->plans) free_plan(cp.p);
         if (c->comm) (void)ncclCommDestroy(c->comm);
         if (c->own) (void)hipStreamDestroy(c->own);
     }

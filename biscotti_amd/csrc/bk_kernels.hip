@@ -222,6 +222,251 @@ __global__ __launch_bounds__(256, 1) void k_gram(const T *__restrict__ X, int64_
 }
 
 // ---------------------------------------------------------------------------
+// K1 v3: LDS-shared split-K Gram (aligned fp64 input; the headline path).
+//
+// Workgroup = 8 waves (2 per SIMD), owns one (group, piece) of the host plan
+// (bk_plan.hip): each wave runs one wave-task -- an off-diagonal 64x64
+// sub-tile (128 accumulator registers), or the two diagonal sub-tiles of a
+// 128-row super-block (upper 16x16 blocks only, 2 x 10 x 8 registers).  The
+// group's <= 8 row-blocks are staged ONCE per workgroup through a 4-deep LDS
+// ring filled by global_load_lds (16 B per lane, 1 KiB = 16 rows x 64 B per
+// instruction, no VGPR staging, 3 k-blocks in flight).  Operands come back by
+// ds_read_b128: lane (rr, g) of row-group q reads row 16q+rr, 16-byte granule
+// g of the 8-column k-block = columns 2g, 2g+1 = MFMA sub-steps s = 0, 1 (the
+// same k permutation for A and B, so the product is X X^T).  Granules are
+// XOR-swizzled by (row >> 1) & 3 on the global SOURCE address (glds writes
+// lane-linearly) and on the read: conflict-free for ds_read_b128.
+// One s_barrier per 8-column k-block (64 MFMAs per SIMD in between).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void g3_issue_stage(const double *__restrict__ X, int64_t ld, int n,
+                                               const int (&blk)[G3_MAXB], int c, int64_t col,
+                                               char *lds_stage, int wave, int lane) {
+    // 4*nb instructions per stage (16 rows each), c = nb/2 per wave
+    const int rq = lane >> 2, j = lane & 3;
+    for (int m = 0; m < c; ++m) {
+        const int i = wave + 8 * m;
+        const int b = i >> 2, ii = i & 3;
+        const int rl = ii * 16 + rq;
+        const int grow = min(blk[b] * 64 + rl, n - 1);
+        const double *src = X + (int64_t)grow * ld + col + 2 * (j ^ ((rl >> 1) & 3));
+        __builtin_amdgcn_global_load_lds((const void *)src,
+                                         (void *)(lds_stage + b * G3_BLK + ii * 1024), 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ d2v g3_frag(const char *lds_blk, int q, int rr, int g) {
+    const int row = q * 16 + rr;
+    return *reinterpret_cast<const d2v *>(lds_blk + row * 64 + 16 * (g ^ ((row >> 1) & 3)));
+}
+
+__device__ __forceinline__ void g3_wait(int vm) {
+    switch (vm) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
+}
+
+__device__ __forceinline__ void g3_barrier() {
+    // every wave's glds for the stage have landed (each waited for its own)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// diagonal sub-tile: upper 16x16 blocks (i <= j) in a flat array of 10
+__device__ __forceinline__ constexpr int dix(int i, int j) { return i * 4 - i * (i - 1) / 2 + (j - i); }
+
+template <int KIND>
+struct G3Acc;
+template <>
+struct G3Acc<T_OFF> {
+    d4v a[4][4];
+};
+template <>
+struct G3Acc<T_PAIR> {
+    d4v a[10], b[10];
+};
+template <>
+struct G3Acc<T_DIAG1> {
+    d4v a[10];
+};
+
+__device__ __forceinline__ void diag_mma(d4v (&acc)[10], const d2v (&a)[4]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i; j < 4; ++j)
+                acc[dix(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][s], a[j][s], acc[dix(i, j)], 0, 0, 0);
+}
+
+__device__ __forceinline__ void g3_load_rows(d2v (&a)[4], const double *__restrict__ X, int64_t ld,
+                                             int n, int b, int64_t c, int64_t d, int rr) {
+    // guarded direct loads for the ragged tail (c = first column of this lane)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double *pr = X + (int64_t)min(b * 64 + q * 16 + rr, n - 1) * ld;
+        a[q].x = c < d ? pr[c] : 0.0;
+        a[q].y = c + 1 < d ? pr[c + 1] : 0.0;
+    }
+}
+
+__device__ __forceinline__ void store_tile(double *out, const d4v (&acc)[4][4], int rr, int g) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = acc[i][j][r];
+}
+
+__device__ __forceinline__ void store_diag(double *out, const d4v (&acc)[10], int rr, int g) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = j >= i ? acc[dix(i, j)][r] : 0.0;
+}
+
+template <int KIND>
+__device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld, int n, int nfull,
+                                        int64_t d, const GroupDesc &G, int p, char *lds, int wave,
+                                        int lane, double *out) {
+    const int rr = lane & 15, g = lane >> 4;
+    int blk[G3_MAXB];
+#pragma unroll
+    for (int b = 0; b < G3_MAXB; ++b) blk[b] = G.blk[b];
+    const int c = G.nb >> 1, P = G.P;
+    const int sA = G.task[wave][1], sB = G.task[wave][2];
+    const int nk = p < nfull ? (nfull - 1 - p) / P + 1 : 0;
+
+    G3Acc<KIND == T_NONE ? T_DIAG1 : KIND> acc;
+    if constexpr (KIND == T_OFF) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc.a[i][j] = d4v{0.0, 0.0, 0.0, 0.0};
+    } else if constexpr (KIND == T_PAIR) {
+#pragma unroll
+        for (int i = 0; i < 10; ++i) acc.a[i] = acc.b[i] = d4v{0.0, 0.0, 0.0, 0.0};
+    } else if constexpr (KIND == T_DIAG1) {
+#pragma unroll
+        for (int i = 0; i < 10; ++i) acc.a[i] = d4v{0.0, 0.0, 0.0, 0.0};
+    }
+
+#pragma unroll
+    for (int s = 0; s < G3_STAGES - 1; ++s)
+        if (s < nk)
+            g3_issue_stage(X, ld, n, blk, c, (int64_t)(p + (int64_t)s * P) * G3_BK,
+                           lds + s * G3_STAGE, wave, lane);
+    for (int t = 0; t < nk; ++t) {
+        const int ahead = min(nk - t - 1, G3_STAGES - 2);  // stages issued after t
+        g3_wait(ahead * c);
+        g3_barrier();
+        if (t + G3_STAGES - 1 < nk)
+            g3_issue_stage(X, ld, n, blk, c, (int64_t)(p + (int64_t)(t + G3_STAGES - 1) * P) * G3_BK,
+                           lds + ((t + G3_STAGES - 1) & (G3_STAGES - 1)) * G3_STAGE, wave, lane);
+        const char *ls = lds + (t & (G3_STAGES - 1)) * G3_STAGE;
+        if constexpr (KIND == T_OFF) {
+            d2v a[4], b[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, rr, g);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[q] = g3_frag(ls + sB * G3_BLK, q, rr, g);
+            gram_mma<false>(acc.a, a, b);
+        } else if constexpr (KIND == T_PAIR) {
+            d2v a[4], b[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, rr, g);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[q] = g3_frag(ls + sB * G3_BLK, q, rr, g);
+            diag_mma(acc.a, a);
+            diag_mma(acc.b, b);
+        } else if constexpr (KIND == T_DIAG1) {
+            d2v a[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, rr, g);
+            diag_mma(acc.a, a);
+        }
+    }
+    if constexpr (KIND != T_NONE) {
+        // ragged tail columns [nfull*8, d): piece 0 of each group, direct loads
+        const int64_t c0 = (int64_t)nfull * G3_BK;
+        if (p == 0 && c0 < d) {
+            const int64_t cc = c0 + 2 * g;
+            d2v a[4], b[4];
+            g3_load_rows(a, X, ld, n, blk[sA], cc, d, rr);
+            g3_load_rows(b, X, ld, n, blk[sB], cc, d, rr);
+            if constexpr (KIND == T_OFF) {
+                gram_mma<false>(acc.a, a, b);
+            } else if constexpr (KIND == T_PAIR) {
+                diag_mma(acc.a, a);
+                diag_mma(acc.b, b);
+            } else {
+                diag_mma(acc.a, a);
+            }
+        }
+        if constexpr (KIND == T_OFF) {
+            store_tile(out, acc.a, rr, g);
+        } else if constexpr (KIND == T_PAIR) {
+            store_diag(out, acc.a, rr, g);
+            store_diag(out + 4096, acc.b, rr, g);
+        } else {
+            store_diag(out, acc.a, rr, g);
+        }
+    }
+}
+
+__global__ __launch_bounds__(512, 2) void k_gram3(const double *__restrict__ X, int64_t ld, int n,
+                                                  int nfull, int64_t d,
+                                                  const GroupDesc *__restrict__ groups,
+                                                  const int *__restrict__ wgtab,
+                                                  double *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int gi = wgtab[2 * blockIdx.x], p = wgtab[2 * blockIdx.x + 1];
+    const GroupDesc &G = groups[gi];
+    double *out = part + ((int64_t)blockIdx.x * 16 + wave * 2) * 4096;
+    switch (G.task[wave][0]) {
+    case T_OFF: g3_wave<T_OFF>(X, ld, n, nfull, d, G, p, lds, wave, lane, out); break;
+    case T_PAIR: g3_wave<T_PAIR>(X, ld, n, nfull, d, G, p, lds, wave, lane, out); break;
+    case T_DIAG1: g3_wave<T_DIAG1>(X, ld, n, nfull, d, G, p, lds, wave, lane, out); break;
+    default: g3_wave<T_NONE>(X, ld, n, nfull, d, G, p, lds, wave, lane, out); break;
+    }
+}
+
+// K1b v3: U[u] = sum over the owning group's pieces (fixed order) of its slab
+__global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part,
+                                                 const int *__restrict__ red,
+                                                 double *__restrict__ U) {
+    const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
+    const int e = chunk * 256 + threadIdx.x;
+    const int64_t first = red[3 * u], np = red[3 * u + 1], stride = red[3 * u + 2];
+    const double *p = part + first * 4096 + e;
+    const int64_t st = stride * 4096;
+    double acc = 0.0;
+    int64_t s = 0;
+    for (; s + 4 <= np; s += 4) {
+        const double v0 = p[(s + 0) * st], v1 = p[(s + 1) * st];
+        const double v2 = p[(s + 2) * st], v3 = p[(s + 3) * st];
+        acc += v0;
+        acc += v1;
+        acc += v2;
+        acc += v3;
+    }
+    for (; s < np; ++s) acc += p[s * st];
+    U[(int64_t)u * 4096 + e] = acc;
+}
+
+// ---------------------------------------------------------------------------
 // K1b: packed upper U[u][64][64] = sum_{s=0..S-1} part[s*ntile+u] (fixed order)
 // grid: ntile*16 blocks of 256 threads (4 rows x 64 cols each)
 // ---------------------------------------------------------------------------
@@ -547,7 +792,23 @@ hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, i
     return hipGetLastError();
 }
 
+hipError_t launch_gram3(const double *X, int64_t ld, int n, int64_t d, const Plan3 &pl,
+                        double *part, hipStream_t st) {
+    hipLaunchKernelGGL(k_gram3, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n, pl.nfull,
+                       d, pl.d_groups, pl.d_wg, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st) {
+    hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 16), dim3(256), 0, st, part, pl.d_red,
+                       U);
+    return hipGetLastError();
+}
+
 hipError_t configure_kernels() {
+    hipError_t e0 = hipFuncSetAttribute((const void *)k_gram3,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
+    if (e0 != hipSuccess) return e0;
     // the row sort may need up to BK_MAX_N * 8 = 128 KiB of dynamic LDS
     hipError_t e = hipFuncSetAttribute((const void *)k_scores<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
