@@ -94,6 +94,7 @@ struct bk_ctx {
     };
     std::vector<CachedPlan> plans;
     int gram_variant = 3;  // 3: LDS-shared v3 for aligned fp64; 1: v1 everywhere (BK_GRAM=v1)
+    int gram_mode = 0;     // BK_GRAM_MODE: timing-only ablations of v3 (tools/, never tests)
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -198,8 +199,9 @@ void free_plan(Plan3 &p) {
     if (p.d_groups) (void)hipFree(p.d_groups);
     if (p.d_wg) (void)hipFree(p.d_wg);
     if (p.d_red) (void)hipFree(p.d_red);
+    if (p.d_wglist) (void)hipFree(p.d_wglist);
     p.d_groups = nullptr;
-    p.d_wg = p.d_red = nullptr;
+    p.d_wg = p.d_red = p.d_wglist = nullptr;
 }
 
 int get_plan3(bk_ctx *c, int64_t n, int64_t d, Plan3 **out) {
@@ -217,11 +219,15 @@ int get_plan3(bk_ctx *c, int64_t n, int64_t d, Plan3 **out) {
     p.T = H.T;
     p.ntile = H.ntile;
     p.ngroups = (int)H.groups.size();
-    p.nwg = (int)H.wg.size() / 2;
+    p.nwg = (int)H.wg.size() / 5;
     p.nfull = H.nfull;
     hipError_t e = hipMalloc(&p.d_groups, H.groups.size() * sizeof(GroupDesc));
     if (e == hipSuccess) e = hipMalloc(&p.d_wg, H.wg.size() * sizeof(int));
     if (e == hipSuccess) e = hipMalloc(&p.d_red, H.red.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&p.d_wglist, H.wglist.size() * sizeof(int));
+    if (e == hipSuccess)
+        e = hipMemcpy(p.d_wglist, H.wglist.data(), H.wglist.size() * sizeof(int),
+                      hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(p.d_groups, H.groups.data(), H.groups.size() * sizeof(GroupDesc),
                       hipMemcpyHostToDevice);
@@ -260,7 +266,8 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
         double *part = (double *)c->part.p;
         const Plan3 &P3 = *p3;
         CHK(timed(c, BK_K_GRAM, [&] {
-            return launch_gram3((const double *)dX, ld, (int)n, d, P3, part, c->stream);
+            return launch_gram3((const double *)dX, ld, (int)n, d, P3, part, c->stream,
+                                c->gram_mode);
         }));
         CHK(timed(c, BK_K_REDUCE, [&] { return launch_reduce3(part, P3, U, c->stream); }));
         return BK_OK;
@@ -372,6 +379,7 @@ int bk_create(bk_ctx **out, int device) {
     c->stream = c->own;
     if (const char *v = getenv("BK_GRAM"))
         if (strcmp(v, "v1") == 0) c->gram_variant = 1;
+    if (const char *v = getenv("BK_GRAM_MODE")) c->gram_mode = atoi(v);
     e = configure_kernels();
     if (e != hipSuccess) {
         (void)hipStreamDestroy(c->own);

@@ -19,26 +19,24 @@ struct Plan {
 };
 
 // K1 v3 (LDS-shared) plan -- DESIGN.md "K1".  Wave-tasks over the 64x64
-// upper sub-tiles: OFF (one off-diagonal sub-tile, 16 MFMA per k-step), PAIR
-// (the two diagonal sub-tiles of a 128-row super-block, upper 16x16 blocks
-// only: 2 x 10 MFMA) and DIAG1 (one diagonal sub-tile, 10).  A group is <= 8
-// wave-tasks over <= 8 row-blocks; one 512-thread workgroup (8 waves, 2 per
-// SIMD) per (group, piece).  Piece p of a group with P pieces takes the
-// 8-column k-blocks p, p+P, p+2P, ... so every workgroup sweeps the columns at
-// the same pace (L2 / Infinity-Cache reuse of blocks shared between groups).
-constexpr int G3_MAXB = 8;    // row-block slots staged per workgroup
-constexpr int G3_BK = 8;      // columns per k-block (one LDS stage)
-constexpr int G3_STAGES = 4;  // LDS ring depth (3 stages in flight)
-constexpr int G3_BLK = 64 * G3_BK * 8;                     // 4096 B per block per stage
-constexpr int G3_STAGE = G3_MAXB * G3_BLK;                 // 32 KiB
-constexpr int G3_LDS = G3_STAGES * G3_STAGE;               // 128 KiB
+// upper sub-tiles: OFF (one off-diagonal sub-tile, 16 MFMA per 4-column
+// k-step), PAIR (the two diagonal sub-tiles of a 128-row super-block, upper
+// 16x16 blocks only: 2 x 10 MFMA) and DIAG1 (one diagonal sub-tile, 10).  A
+// group is <= 8 wave-tasks over <= 6 row-blocks; one 512-thread workgroup (8
+// waves, 2 per SIMD) per (group, XCD, slice); see bk_plan.hip.
+constexpr int G3_MAXB = 6;    // row-block slots staged per workgroup
+constexpr int G3_BK = 16;     // columns per k-block (one LDS stage, 128 B per row)
+constexpr int G3_STAGES = 3;  // LDS ring depth (2 k-blocks in flight)
+constexpr int G3_BLK = 64 * G3_BK * 8;                     // 8 KiB per block per stage
+constexpr int G3_STAGE = G3_MAXB * G3_BLK;                 // 48 KiB
+constexpr int G3_LDS = G3_STAGES * G3_STAGE;               // 144 KiB
 enum { T_NONE = 0, T_OFF = 1, T_PAIR = 2, T_DIAG1 = 3 };
 
 struct GroupDesc {
     int nb;               // row-blocks staged (even; padded with a duplicate)
     int blk[G3_MAXB];     // 64-row block index per slot
-    int P;                // pieces of this group (k-block stride)
-    int wg0;              // first workgroup of this group
+    int Q;                // workgroups of this group per XCD
+    int wg0;              // offset of this group's list in wglist
     int cost;             // max over SIMDs of its two waves' MFMA units per k-step
     int task[8][5];       // per wave: {kind, slotA, slotB, u0, u1}
 };
@@ -47,21 +45,23 @@ struct Plan3 {
     int n = 0, T = 0, ntile = 0, ngroups = 0, nwg = 0, nfull = 0;
     int64_t d = 0;
     GroupDesc *d_groups = nullptr;  // device copies (owned by the context)
-    int *d_wg = nullptr;            // per workgroup: {group, piece}
-    int *d_red = nullptr;           // per sub-tile u: {first slab, npieces, slab stride}
+    int *d_wg = nullptr;            // per workgroup: {group, kstart, kstride, kend, tail}
+    int *d_red = nullptr;           // per sub-tile u: {list offset, count, slot}
+    int *d_wglist = nullptr;        // per group: its workgroups, in reduction order
 };
 
 // host planner (bk_plan.hip)
 struct Plan3Host {
     int T = 0, ntile = 0, nfull = 0;
     std::vector<GroupDesc> groups;
-    std::vector<int> wg;   // 2 per workgroup
-    std::vector<int> red;  // 3 per sub-tile
+    std::vector<int> wg;      // 5 per workgroup
+    std::vector<int> red;     // 3 per sub-tile
+    std::vector<int> wglist;  // concatenated per-group workgroup lists
 };
 Plan3Host build_plan3(int n, int64_t d, int num_cu);
 
 hipError_t launch_gram3(const double *X, int64_t ld, int n, int64_t d, const Plan3 &pl,
-                        double *part, hipStream_t st);
+                        double *part, hipStream_t st, int mode = 0);
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st);
 hipError_t configure_kernels();
 hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan &pl,

@@ -238,25 +238,9 @@ __global__ __launch_bounds__(256, 1) void k_gram(const T *__restrict__ X, int64_
 // lane-linearly) and on the read: conflict-free for ds_read_b128.
 // One s_barrier per 8-column k-block (64 MFMAs per SIMD in between).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void g3_issue_stage(const double *__restrict__ X, int64_t ld, int n,
-                                               const int (&blk)[G3_MAXB], int c, int64_t col,
-                                               char *lds_stage, int wave, int lane) {
-    // 4*nb instructions per stage (16 rows each), c = nb/2 per wave
-    const int rq = lane >> 2, j = lane & 3;
-    for (int m = 0; m < c; ++m) {
-        const int i = wave + 8 * m;
-        const int b = i >> 2, ii = i & 3;
-        const int rl = ii * 16 + rq;
-        const int grow = min(blk[b] * 64 + rl, n - 1);
-        const double *src = X + (int64_t)grow * ld + col + 2 * (j ^ ((rl >> 1) & 3));
-        __builtin_amdgcn_global_load_lds((const void *)src,
-                                         (void *)(lds_stage + b * G3_BLK + ii * 1024), 16, 0, 0);
-    }
-}
-
-__device__ __forceinline__ d2v g3_frag(const char *lds_blk, int q, int rr, int g) {
+__device__ __forceinline__ d2v g3_frag(const char *lds_blk, int q, int h, int rr, int g) {
     const int row = q * 16 + rr;
-    return *reinterpret_cast<const d2v *>(lds_blk + row * 64 + 16 * (g ^ ((row >> 1) & 3)));
+    return *reinterpret_cast<const d2v *>(lds_blk + row * 128 + 16 * ((4 * h + g) ^ (row & 7)));
 }
 
 __device__ __forceinline__ void g3_wait(int vm) {
@@ -266,8 +250,14 @@ __device__ __forceinline__ void g3_wait(int vm) {
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
     case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     }
 }
 
@@ -336,17 +326,61 @@ __device__ __forceinline__ void store_diag(double *out, const d4v (&acc)[10], in
                 out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = j >= i ? acc[dix(i, j)][r] : 0.0;
 }
 
-template <int KIND>
+// one MFMA sub-step s (columns 2g+s of the k-block) of an off-diagonal tile
+template <int S>
+__device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const d2v (&a)[4], const d2v (&b)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][S], b[j][S], acc[i][j], 0, 0, 0);
+}
+// STAG: waves 4-7 (the SIMD partners of waves 0-3) run their OFF tile half a
+// k-block behind -- the second 8-column half of block t-1 is issued after the
+// barrier of block t, from registers -- so that after every barrier one wave
+// of each SIMD has MFMAs ready while its partner waits for its LDS reads.  The
+// accumulation order (block by block, column by column) is unchanged, so the
+// result is bitwise identical to the unstaggered schedule.
+template <int KIND, int MODE, bool STAG>
 __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld, int n, int nfull,
-                                        int64_t d, const GroupDesc &G, int p, char *lds, int wave,
-                                        int lane, double *out) {
+                                        int64_t d, const GroupDesc &G, const int *wd, char *lds,
+                                        int wave, int lane, double *out) {
     const int rr = lane & 15, g = lane >> 4;
     int blk[G3_MAXB];
 #pragma unroll
     for (int b = 0; b < G3_MAXB; ++b) blk[b] = G.blk[b];
-    const int c = G.nb >> 1, P = G.P;
+    const int c = G.nb;  // glds per wave per k-block (8 per row-block, 8 waves)
     const int sA = G.task[wave][1], sB = G.task[wave][2];
-    const int nk = p < nfull ? (nfull - 1 - p) / P + 1 : 0;
+    const int kst = wd[1], kstr = wd[2], kend = wd[3];
+    const int nk = kst < kend ? (kend - 1 - kst) / kstr + 1 : 0;
+
+    // this wave's c (<= 6) glds per k-block: fixed per-lane row pointers and LDS
+    // offsets; a stage only adds the k-block's column.  Instruction i of a stage
+    // moves rows 8ii..8ii+7 (128 B each) of slot b = i/8; lane L takes row
+    // 8ii + L/8, granule (L&7) of the LDS row <- global granule (L&7)^(row&7).
+    const double *gsrc[G3_MAXB];
+    int gdst[G3_MAXB];
+    {
+        const int rq = lane >> 3, j = lane & 7;
+#pragma unroll
+        for (int m = 0; m < G3_MAXB; ++m) {
+            const int i = wave + 8 * m;
+            const int b = i >> 3, ii = i & 7;
+            const int rl = ii * 8 + rq;
+            const int grow = min(blk[b] * 64 + rl, n - 1);
+            gsrc[m] = X + (int64_t)grow * ld + 2 * (j ^ (rl & 7));
+            gdst[m] = b * G3_BLK + ii * 1024;
+        }
+    }
+    auto issue = [&](int64_t kb, int stage) {
+        const int64_t col = kb * G3_BK;
+        char *base = lds + stage * G3_STAGE;
+#pragma unroll
+        for (int m = 0; m < G3_MAXB; ++m)
+            if (m < c)
+                __builtin_amdgcn_global_load_lds((const void *)(gsrc[m] + col),
+                                                 (void *)(base + gdst[m]), 16, 0, 0);
+    };
 
     G3Acc<KIND == T_NONE ? T_DIAG1 : KIND> acc;
     if constexpr (KIND == T_OFF) {
@@ -361,57 +395,104 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
 #pragma unroll
         for (int i = 0; i < 10; ++i) acc.a[i] = d4v{0.0, 0.0, 0.0, 0.0};
     }
+    d2v ha[4], hb[4];  // STAG: the held second half of the previous k-block
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ha[q] = hb[q] = d2v{0.0, 0.0};
 
 #pragma unroll
     for (int s = 0; s < G3_STAGES - 1; ++s)
-        if (s < nk)
-            g3_issue_stage(X, ld, n, blk, c, (int64_t)(p + (int64_t)s * P) * G3_BK,
-                           lds + s * G3_STAGE, wave, lane);
+        if (s < nk && MODE != 2) issue(kst + (int64_t)s * kstr, s);
+    int buf = 0;
     for (int t = 0; t < nk; ++t) {
         const int ahead = min(nk - t - 1, G3_STAGES - 2);  // stages issued after t
-        g3_wait(ahead * c);
+        g3_wait(MODE == 2 ? 0 : ahead * c);
         g3_barrier();
-        if (t + G3_STAGES - 1 < nk)
-            g3_issue_stage(X, ld, n, blk, c, (int64_t)(p + (int64_t)(t + G3_STAGES - 1) * P) * G3_BK,
-                           lds + ((t + G3_STAGES - 1) & (G3_STAGES - 1)) * G3_STAGE, wave, lane);
-        const char *ls = lds + (t & (G3_STAGES - 1)) * G3_STAGE;
-        if constexpr (KIND == T_OFF) {
-            d2v a[4], b[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, rr, g);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) b[q] = g3_frag(ls + sB * G3_BLK, q, rr, g);
-            gram_mma<false>(acc.a, a, b);
-        } else if constexpr (KIND == T_PAIR) {
-            d2v a[4], b[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, rr, g);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) b[q] = g3_frag(ls + sB * G3_BLK, q, rr, g);
-            diag_mma(acc.a, a);
-            diag_mma(acc.b, b);
-        } else if constexpr (KIND == T_DIAG1) {
-            d2v a[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, rr, g);
-            diag_mma(acc.a, a);
+        const char *ls = lds + buf * G3_STAGE;
+        const int nbuf = buf == 0 ? G3_STAGES - 1 : buf - 1;  // (t + STAGES - 1) % STAGES
+        const bool more = t + G3_STAGES - 1 < nk && MODE != 2;
+        const int64_t nkb = kst + (int64_t)(t + G3_STAGES - 1) * kstr;
+        buf = buf == G3_STAGES - 1 ? 0 : buf + 1;
+        if constexpr (MODE == 1) {
+            if (more) issue(nkb, nbuf);
+            continue;
         }
-    }
-    if constexpr (KIND != T_NONE) {
-        // ragged tail columns [nfull*8, d): piece 0 of each group, direct loads
-        const int64_t c0 = (int64_t)nfull * G3_BK;
-        if (p == 0 && c0 < d) {
-            const int64_t cc = c0 + 2 * g;
-            d2v a[4], b[4];
-            g3_load_rows(a, X, ld, n, blk[sA], cc, d, rr);
-            g3_load_rows(b, X, ld, n, blk[sB], cc, d, rr);
-            if constexpr (KIND == T_OFF) {
-                gram_mma<false>(acc.a, a, b);
-            } else if constexpr (KIND == T_PAIR) {
+        if constexpr (KIND == T_OFF) {
+            d2v a0[4], b0[4], a1[4], b1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a0[q] = g3_frag(ls + sA * G3_BLK, q, 0, rr, g);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b0[q] = g3_frag(ls + sB * G3_BLK, q, 0, rr, g);
+            if constexpr (STAG) {
+                if (t > 0) {
+                    off_mma<0>(acc.a, ha, hb);
+                    off_mma<1>(acc.a, ha, hb);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a1[q] = g3_frag(ls + sA * G3_BLK, q, 1, rr, g);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b1[q] = g3_frag(ls + sB * G3_BLK, q, 1, rr, g);
+            if (more) issue(nkb, nbuf);
+            off_mma<0>(acc.a, a0, b0);
+            off_mma<1>(acc.a, a0, b0);
+            if constexpr (STAG) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    ha[q] = a1[q];
+                    hb[q] = b1[q];
+                }
+            } else {
+                off_mma<0>(acc.a, a1, b1);
+                off_mma<1>(acc.a, a1, b1);
+            }
+        } else if constexpr (KIND == T_PAIR) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                d2v a[4], b[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, h, rr, g);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) b[q] = g3_frag(ls + sB * G3_BLK, q, h, rr, g);
+                if (h == 0 && more) issue(nkb, nbuf);
                 diag_mma(acc.a, a);
                 diag_mma(acc.b, b);
-            } else {
+            }
+        } else if constexpr (KIND == T_DIAG1) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                d2v a[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, h, rr, g);
+                if (h == 0 && more) issue(nkb, nbuf);
                 diag_mma(acc.a, a);
+            }
+        } else {
+            if (more) issue(nkb, nbuf);
+        }
+    }
+    if constexpr (KIND == T_OFF && STAG && MODE != 1)
+        if (nk > 0) {
+            off_mma<0>(acc.a, ha, hb);
+            off_mma<1>(acc.a, ha, hb);
+        }
+    if constexpr (KIND != T_NONE) {
+        // ragged tail columns [nfull*16, d): one workgroup per group, direct loads
+        const int64_t c0 = (int64_t)nfull * G3_BK;
+        if (wd[4] && c0 < d) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int64_t cc = c0 + 8 * h + 2 * g;
+                d2v a[4], b[4];
+                g3_load_rows(a, X, ld, n, blk[sA], cc, d, rr);
+                g3_load_rows(b, X, ld, n, blk[sB], cc, d, rr);
+                if constexpr (KIND == T_OFF) {
+                    gram_mma<false>(acc.a, a, b);
+                } else if constexpr (KIND == T_PAIR) {
+                    diag_mma(acc.a, a);
+                    diag_mma(acc.b, b);
+                } else {
+                    diag_mma(acc.a, a);
+                }
             }
         }
         if constexpr (KIND == T_OFF) {
@@ -425,6 +506,10 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
     }
 }
 
+#ifndef G3_STAGGER
+#define G3_STAGGER 1
+#endif
+template <int MODE>
 __global__ __launch_bounds__(512, 2) void k_gram3(const double *__restrict__ X, int64_t ld, int n,
                                                   int nfull, int64_t d,
                                                   const GroupDesc *__restrict__ groups,
@@ -432,37 +517,44 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const double *__restrict__ X, 
                                                   double *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int gi = wgtab[2 * blockIdx.x], p = wgtab[2 * blockIdx.x + 1];
-    const GroupDesc &G = groups[gi];
+    const int *wd = wgtab + 5 * blockIdx.x;
+    const GroupDesc &G = groups[wd[0]];
     double *out = part + ((int64_t)blockIdx.x * 16 + wave * 2) * 4096;
     switch (G.task[wave][0]) {
-    case T_OFF: g3_wave<T_OFF>(X, ld, n, nfull, d, G, p, lds, wave, lane, out); break;
-    case T_PAIR: g3_wave<T_PAIR>(X, ld, n, nfull, d, G, p, lds, wave, lane, out); break;
-    case T_DIAG1: g3_wave<T_DIAG1>(X, ld, n, nfull, d, G, p, lds, wave, lane, out); break;
-    default: g3_wave<T_NONE>(X, ld, n, nfull, d, G, p, lds, wave, lane, out); break;
+    case T_OFF:
+        if (wave >= 4 && G3_STAGGER)
+            g3_wave<T_OFF, MODE, true>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out);
+        else
+            g3_wave<T_OFF, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out);
+        break;
+    case T_PAIR: g3_wave<T_PAIR, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out); break;
+    case T_DIAG1: g3_wave<T_DIAG1, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out); break;
+    default: g3_wave<T_NONE, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out); break;
     }
 }
 
-// K1b v3: U[u] = sum over the owning group's pieces (fixed order) of its slab
+// K1b v3: U[u] = sum over the owning group's workgroups (fixed order) of its slab
 __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part,
                                                  const int *__restrict__ red,
+                                                 const int *__restrict__ wglist,
                                                  double *__restrict__ U) {
     const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
     const int e = chunk * 256 + threadIdx.x;
-    const int64_t first = red[3 * u], np = red[3 * u + 1], stride = red[3 * u + 2];
-    const double *p = part + first * 4096 + e;
-    const int64_t st = stride * 4096;
+    const int off = red[3 * u], np = red[3 * u + 1], slot = red[3 * u + 2];
+    const int *wl = wglist + off;
     double acc = 0.0;
-    int64_t s = 0;
+    int s = 0;
     for (; s + 4 <= np; s += 4) {
-        const double v0 = p[(s + 0) * st], v1 = p[(s + 1) * st];
-        const double v2 = p[(s + 2) * st], v3 = p[(s + 3) * st];
+        const double v0 = part[((int64_t)wl[s + 0] * 16 + slot) * 4096 + e];
+        const double v1 = part[((int64_t)wl[s + 1] * 16 + slot) * 4096 + e];
+        const double v2 = part[((int64_t)wl[s + 2] * 16 + slot) * 4096 + e];
+        const double v3 = part[((int64_t)wl[s + 3] * 16 + slot) * 4096 + e];
         acc += v0;
         acc += v1;
         acc += v2;
         acc += v3;
     }
-    for (; s < np; ++s) acc += p[s * st];
+    for (; s < np; ++s) acc += part[((int64_t)wl[s] * 16 + slot) * 4096 + e];
     U[(int64_t)u * 4096 + e] = acc;
 }
 
@@ -793,22 +885,32 @@ hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, i
 }
 
 hipError_t launch_gram3(const double *X, int64_t ld, int n, int64_t d, const Plan3 &pl,
-                        double *part, hipStream_t st) {
-    hipLaunchKernelGGL(k_gram3, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n, pl.nfull,
-                       d, pl.d_groups, pl.d_wg, part);
+                        double *part, hipStream_t st, int mode) {
+    // mode != 0: timing-only ablations (1: no MFMA, 2: no global loads) -- wrong results
+    if (mode == 1)
+        hipLaunchKernelGGL(k_gram3<1>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
+                           pl.nfull, d, pl.d_groups, pl.d_wg, part);
+    else if (mode == 2)
+        hipLaunchKernelGGL(k_gram3<2>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
+                           pl.nfull, d, pl.d_groups, pl.d_wg, part);
+    else
+        hipLaunchKernelGGL(k_gram3<0>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
+                           pl.nfull, d, pl.d_groups, pl.d_wg, part);
     return hipGetLastError();
 }
 
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st) {
     hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 16), dim3(256), 0, st, part, pl.d_red,
-                       U);
+                       pl.d_wglist, U);
     return hipGetLastError();
 }
 
 hipError_t configure_kernels() {
-    hipError_t e0 = hipFuncSetAttribute((const void *)k_gram3,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
-    if (e0 != hipSuccess) return e0;
+    for (const void *k : {(const void *)k_gram3<0>, (const void *)k_gram3<1>,
+                          (const void *)k_gram3<2>}) {
+        hipError_t e0 = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
+        if (e0 != hipSuccess) return e0;
+    }
     // the row sort may need up to BK_MAX_N * 8 = 128 KiB of dynamic LDS
     hipError_t e = hipFuncSetAttribute((const void *)k_scores<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 131072);

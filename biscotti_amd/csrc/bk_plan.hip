@@ -1,12 +1,14 @@
 // bk_plan.hip -- host planner for K1 v3 (see bk_internal.h and DESIGN.md "K1").
 //
 // Turns (n, d, #CUs) into: wave-tasks over the 64x64 upper sub-tiles of the
-// Gram, groups of <= 8 tasks sharing <= 8 row-blocks (one 512-thread
-// workgroup each), and a per-group piece count P that balances the groups'
-// per-SIMD MFMA cost so that every workgroup of a launch finishes together.
+// Gram, groups of <= 8 tasks sharing <= 6 row-blocks (one 512-thread
+// workgroup each), and per-XCD slices of the columns whose counts balance the
+// groups' per-SIMD MFMA cost so that the workgroups of a launch finish
+// together.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdint>
 #include <functional>
 #include <queue>
@@ -72,7 +74,6 @@ GroupDesc make_group(int T, const std::vector<Task> &tasks) {
         }
     }
     if (blocks.empty()) blocks.push_back(0);
-    if (blocks.size() & 1) blocks.push_back(blocks[0]);  // glds issue needs an even count
     G.nb = (int)blocks.size();
     for (int i = 0; i < G3_MAXB; ++i) G.blk[i] = i < G.nb ? blocks[i] : blocks[0];
     G.cost = group_cost(tasks);
@@ -84,57 +85,85 @@ GroupDesc make_group(int T, const std::vector<Task> &tasks) {
 Plan3Host build_plan3(int n, int64_t d, int num_cu) {
     Plan3Host H;
     const int T = (n + 63) / 64;
-    const int TT = (T + 1) / 2;
+    const int TT = (T + 1) / 2;  // 128-row super-blocks
     H.T = T;
     H.ntile = T * (T + 1) / 2;
     H.nfull = (int)(d / G3_BK);
 
     std::vector<std::vector<Task>> groups;  // each: 8 wave slots (waves w, w+4 pair on a SIMD)
-
-    // (1) the diagonal band, 4 super-blocks per group: PAIR tasks on waves 0-3,
-    //     the near-diagonal OFF sub-tile (2I, 2I+1) on waves 4-7 -> 20 + 16 per SIMD
-    for (int I0 = 0; I0 < TT; I0 += 4) {
-        std::vector<Task> w(8, Task{T_NONE, 0, 0, 0});
-        for (int k = 0; k < 4 && I0 + k < TT; ++k) {
-            const int b0 = 2 * (I0 + k), b1 = b0 + 1;
-            if (b1 < T) {
-                w[k] = Task{T_PAIR, b0, b1, COST_PAIR};
-                w[k + 4] = Task{T_OFF, b0, b1, COST_OFF};
-            } else {
-                w[k] = Task{T_DIAG1, b0, b0, COST_DIAG1};
+    const Task none{T_NONE, 0, 0, 0};
+    auto diag_task = [&](int I) {  // the diagonal sub-tiles of super-block I
+        const int b0 = 2 * I, b1 = b0 + 1;
+        return b1 < T ? Task{T_PAIR, b0, b1, COST_PAIR} : Task{T_DIAG1, b0, b0, COST_DIAG1};
+    };
+    auto near_task = [&](int I) {  // the off-diagonal sub-tile inside super-block I
+        const int b0 = 2 * I, b1 = b0 + 1;
+        return b1 < T ? Task{T_OFF, b0, b1, COST_OFF} : none;
+    };
+    auto super_tasks = [&](int I, int J) {  // the <= 4 OFF sub-tiles of super-tile (I < J)
+        std::vector<Task> st;
+        for (int a = 0; a < 2; ++a)
+            for (int b = 0; b < 2; ++b) {
+                const int bi = 2 * I + a, bj = 2 * J + b;
+                if (bi < T && bj < T) st.push_back(Task{T_OFF, bi, bj, COST_OFF});
             }
-        }
+        return st;
+    };
+    // (1) the diagonal band in "quads" of two super-blocks (4 row-blocks):
+    //     waves 0,1: PAIR tasks, 4,5: the near-diagonal OFF tasks (20 + 16 per
+    //     SIMD), 2,3,6,7: the off-diagonal super-tile (I, I+1) between them
+    std::vector<char> used((size_t)TT * TT, 0);
+    for (int I = 0; I + 1 < TT; I += 2) {
+        std::vector<Task> w(8, none);
+        w[0] = diag_task(I);
+        w[1] = diag_task(I + 1);
+        w[4] = near_task(I);
+        w[5] = near_task(I + 1);
+        const std::vector<Task> st = super_tasks(I, I + 1);
+        const int slots[4] = {2, 3, 6, 7};
+        for (size_t k = 0; k < st.size(); ++k) w[slots[k]] = st[k];
+        used[(size_t)I * TT + I + 1] = 1;
         groups.push_back(w);
     }
-    // (2) off-diagonal super-tiles (I < J): 4 OFF tasks each; two super-tiles of
-    //     the same super-row per group (6 row-blocks), leftovers paired (<= 8)
-    std::vector<std::vector<Task>> singles;
+    if (TT & 1) {  // a last lone super-block
+        std::vector<Task> w(8, none);
+        w[0] = diag_task(TT - 1);
+        w[4] = near_task(TT - 1);
+        groups.push_back(w);
+    }
+    // (2) the other off-diagonal super-tiles, two per group along a super-row
+    //     (6 row-blocks); leftovers paired when they share a super-block
+    std::vector<std::pair<int, int>> singles;
     for (int I = 0; I < TT; ++I) {
-        std::vector<std::vector<Task>> row;
-        for (int J = I + 1; J < TT; ++J) {
-            std::vector<Task> st;
-            for (int a = 0; a < 2; ++a)
-                for (int b = 0; b < 2; ++b) {
-                    const int bi = 2 * I + a, bj = 2 * J + b;
-                    if (bi < T && bj < T) st.push_back(Task{T_OFF, bi, bj, COST_OFF});
-                }
-            row.push_back(st);
-        }
+        std::vector<int> row;
+        for (int J = I + 1; J < TT; ++J)
+            if (!used[(size_t)I * TT + J]) row.push_back(J);
         for (size_t k = 0; k + 1 < row.size(); k += 2) {
-            std::vector<Task> w = row[k];
-            w.resize(4, Task{T_NONE, 0, 0, 0});
-            for (const Task &t : row[k + 1]) w.push_back(t);
-            w.resize(8, Task{T_NONE, 0, 0, 0});
+            std::vector<Task> w = super_tasks(I, row[k]);
+            w.resize(4, none);
+            for (const Task &t : super_tasks(I, row[k + 1])) w.push_back(t);
+            w.resize(8, none);
             groups.push_back(w);
         }
-        if (row.size() & 1) singles.push_back(row.back());
+        if (row.size() & 1) singles.push_back({I, row.back()});
     }
-    for (size_t k = 0; k < singles.size(); k += 2) {
-        std::vector<Task> w = singles[k];
-        w.resize(4, Task{T_NONE, 0, 0, 0});
-        if (k + 1 < singles.size())
-            for (const Task &t : singles[k + 1]) w.push_back(t);
-        w.resize(8, Task{T_NONE, 0, 0, 0});
+    std::vector<char> taken(singles.size(), 0);
+    for (size_t a = 0; a < singles.size(); ++a) {
+        if (taken[a]) continue;
+        taken[a] = 1;
+        std::vector<Task> w = super_tasks(singles[a].first, singles[a].second);
+        w.resize(4, none);
+        for (size_t b = a + 1; b < singles.size(); ++b) {
+            if (taken[b]) continue;
+            const auto &x = singles[a], &y = singles[b];
+            if (x.first == y.first || x.first == y.second || x.second == y.first ||
+                x.second == y.second) {
+                taken[b] = 1;
+                for (const Task &t : super_tasks(y.first, y.second)) w.push_back(t);
+                break;
+            }
+        }
+        w.resize(8, none);
         groups.push_back(w);
     }
 
@@ -142,51 +171,91 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu) {
     for (auto &w : groups) G.push_back(make_group(T, w));
     const int ng = (int)G.size();
 
-    // (3) pieces: P_g ~ cost_g so per-WG time ~ (k-blocks / P_g) * cost_g is even;
-    //     pick the total that minimises the simulated makespan on num_cu slots
+    // (3) XCD-aware pieces.  Workgroups b and b+8 share an XCD (dispatch is
+    //     round-robin; speed only, never correctness).  XCD x owns k-blocks
+    //     [K_x, K_x+1); each group g runs Q_g workgroups per XCD, workgroup q
+    //     taking k-blocks K_x + q, + Q_g, ... so all groups on an XCD sweep the
+    //     same columns together and re-read shared row-blocks from its L2.
+    //     Q_g ~ cost_g (per-SIMD MFMA units per k-block) balances the groups.
     const int nfull = H.nfull;
+    constexpr int NX = 8;
+    const int per_xcd = std::max(1, num_cu / NX);
+    std::vector<int64_t> K(NX + 1);
+    for (int x = 0; x <= NX; ++x) K[x] = (int64_t)nfull * x / NX;
     double csum = 0;
     for (auto &g : G) csum += g.cost;
-    const double wg_overhead = 64.0 * 16.0;  // prologue + slab write, in cost*k-block units
+    const double wg_overhead = 64.0 * 24.0;  // prologue + slab write, in cost * k-block units
     double best = 1e300;
-    std::vector<int> bestP(ng, 1);
-    for (int mult : {1, 2, 3, 4, 6, 8, 12, 16}) {
-        const double target = (double)mult * num_cu;
-        std::vector<int> P(ng);
+    std::vector<int> bestQ(ng, 1);
+    for (int rounds = 1; rounds <= 16; rounds *= 2) {
+        const double slots_total = (double)rounds * per_xcd;
+        if (ng > slots_total * 4) continue;
+        // largest-remainder apportionment of the XCD's slots, Q_g >= 1
+        std::vector<int> Q(ng);
+        std::vector<std::pair<double, int>> rem;
+        int used = 0;
         for (int g = 0; g < ng; ++g) {
-            int p = (int)(target * G[g].cost / csum + 0.5);
-            p = std::max(1, std::min(p, std::max(1, nfull)));
-            P[g] = p;
+            const double want = slots_total * G[g].cost / csum;
+            Q[g] = std::max(1, (int)want);
+            used += Q[g];
+            rem.push_back({want - (int)want, g});
         }
-        // list-schedule in launch order on num_cu slots (1 workgroup per CU)
-        std::priority_queue<double, std::vector<double>, std::greater<double>> slots;
-        for (int i = 0; i < num_cu; ++i) slots.push(0.0);
-        double mk = 0;
+        std::sort(rem.begin(), rem.end(), [](auto &a, auto &b) { return a.first > b.first; });
+        for (size_t i = 0; i < rem.size() && used < (int)slots_total; ++i, ++used) Q[rem[i].second]++;
+        // list-schedule one XCD's workgroups (largest first) on per_xcd slots
+        std::vector<double> jobs;
+        const int64_t R = K[1] - K[0];
         for (int g = 0; g < ng; ++g)
-            for (int p = 0; p < P[g]; ++p) {
-                const int nk = p < nfull ? (nfull - 1 - p) / P[g] + 1 : 0;
-                const double t0 = slots.top();
-                slots.pop();
-                const double t1 = t0 + (double)nk * G[g].cost + wg_overhead;
-                mk = std::max(mk, t1);
-                slots.push(t1);
+            for (int q = 0; q < Q[g]; ++q) {
+                const int64_t nk = q < R ? (R - 1 - q) / Q[g] + 1 : 0;
+                jobs.push_back((double)nk * G[g].cost + wg_overhead);
             }
+        std::priority_queue<double, std::vector<double>, std::greater<double>> slots;
+        for (int i = 0; i < per_xcd; ++i) slots.push(0.0);
+        double mk = 0;
+        for (double j : jobs) {
+            const double t1 = slots.top() + j;
+            slots.pop();
+            slots.push(t1);
+            mk = std::max(mk, t1);
+        }
         if (mk < best * 0.995) {
             best = mk;
-            bestP = P;
+            bestQ = Q;
         }
     }
-    int wg = 0;
+    // per-XCD launch lists, interleaved over groups; b = 8 j + x
+    std::vector<std::vector<std::array<int, 5>>> lists(NX);
+    int maxq = 0;
+    for (int g = 0; g < ng; ++g) maxq = std::max(maxq, bestQ[g]);
+    for (int x = 0; x < NX; ++x)
+        for (int q = 0; q < maxq; ++q)
+            for (int g = 0; g < ng; ++g)
+                if (q < bestQ[g])
+                    lists[x].push_back({g, (int)(K[x] + q), bestQ[g], (int)K[x + 1],
+                                        (x == 0 && q == 0) ? 1 : 0});
+    size_t maxlen = 0;
+    for (auto &l : lists) maxlen = std::max(maxlen, l.size());
+    std::vector<std::vector<int>> gw(ng);
+    for (size_t j = 0; j < maxlen; ++j)
+        for (int x = 0; x < NX; ++x) {
+            const int b = (int)(H.wg.size() / 5);
+            if (j < lists[x].size()) {
+                const auto &e = lists[x][j];
+                H.wg.insert(H.wg.end(), e.begin(), e.end());
+                gw[e[0]].push_back(b);
+            } else {
+                // keep b = 8j + x: an empty workgroup (no k-blocks) of group 0
+                H.wg.insert(H.wg.end(), {0, 0, 1, 0, 0});
+                gw[0].push_back(b);
+            }
+        }
     for (int g = 0; g < ng; ++g) {
-        G[g].P = bestP[g];
-        G[g].wg0 = wg;
-        for (int p = 0; p < bestP[g]; ++p) {
-            H.wg.push_back(g);
-            H.wg.push_back(p);
-        }
-        wg += bestP[g];
+        G[g].Q = bestQ[g];
+        G[g].wg0 = (int)H.wglist.size();
+        H.wglist.insert(H.wglist.end(), gw[g].begin(), gw[g].end());
     }
-    // (4) reduce table: sub-tile u -> its slabs (wg0 + p) * 16 + wave * 2 + t
+    // (4) reduce table: sub-tile u -> its group's workgroups, slot wave * 2 + t
     H.red.assign((size_t)H.ntile * 3, 0);
     std::vector<int> seen(H.ntile, 0);
     for (int g = 0; g < ng; ++g)
@@ -194,13 +263,15 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu) {
             for (int t = 0; t < 2; ++t) {
                 const int u = G[g].task[w][3 + t];
                 if (u < 0) continue;
-                H.red[3 * u] = G[g].wg0 * 16 + w * 2 + t;
-                H.red[3 * u + 1] = G[g].P;
-                H.red[3 * u + 2] = 16;
+                H.red[3 * u] = G[g].wg0;
+                H.red[3 * u + 1] = (int)gw[g].size();
+                H.red[3 * u + 2] = w * 2 + t;
                 seen[u]++;
             }
+    bool ok = true;
+    for (auto &g : G) ok = ok && g.nb <= G3_MAXB;
     for (int u = 0; u < H.ntile; ++u)
-        if (seen[u] != 1) H.red[3 * u + 1] = -1;  // planner bug marker (checked by the caller)
+        if (seen[u] != 1 || !ok) H.red[3 * u + 1] = -1;  // planner bug marker (checked by the caller)
     H.groups = G;
     return H;
 }
