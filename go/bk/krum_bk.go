@@ -1,0 +1,107 @@
+// Package main (drop-in file for DistributedML/Biscotti DistSys/).
+//
+// krum_bk.go replaces the go-python Multi-Krum call of DistSys/krum.go with the
+// MI355X engine libbk.so (include/bk.h).  It keeps the verifier call surface:
+//
+//	func (krumval *KRUMValidator) initialize()                        krum.go:31-44
+//	func (krumval *KRUMValidator) getTopKRUMIndex(deltas [][]float64) []int
+//	                                                                  krum.go:100-166
+//
+// computeScores (krum.go:77-98), VerifyUpdateKRUM (:227-365),
+// startKRUMDeadlineTimer (:178-224) and checkIfAccepted (:47-73) are unchanged.
+// To adopt it: delete getTopKRUMIndex/initialize (and the pyKRUMFunc global)
+// from krum.go, add this file, build with
+//
+//	CGO_CFLAGS="-I<repo>/include" CGO_LDFLAGS="-L<repo>/biscotti_amd -lbk -Wl,-rpath,<repo>/biscotti_amd" go build
+//
+// NOT BUILT IN THIS REPOSITORY: the build image has no Go toolchain (see
+// INTEGRATION.md).  The C calls it makes are exercised from Python through the
+// same ABI (tests/test_abi.py, tests/test_gpu_parity.py).
+package main
+
+/*
+#cgo LDFLAGS: -lbk
+#include <stdlib.h>
+#include <string.h>
+#include "bk.h"
+*/
+import "C"
+
+import (
+	"unsafe"
+)
+
+var (
+	bkCtx      *C.bk_ctx
+	bkStage    unsafe.Pointer // C-owned pinned staging (cgo may not keep Go pointers)
+	bkStageLen int64
+)
+
+// initialize binds the engine instead of pyKRUMFunc (krum.go:31-44).
+func (krumval *KRUMValidator) initialize() {
+	if bkCtx != nil {
+		return
+	}
+	var ctx *C.bk_ctx
+	if st := C.bk_create(&ctx, 0); st != C.BK_OK {
+		outLog.Printf("bk_create failed (%d): %s", int(st), C.GoString(C.bk_last_error()))
+		return
+	}
+	bkCtx = ctx
+	outLog.Printf("Krum engine: libbk ABI %d", int(C.bk_abi_version()))
+}
+
+// getTopKRUMIndex keeps the signature and the clip rule of krum.go:100-166:
+// adversaryCount := int(NumAdversaries * float64(n)); the accepted indices
+// index the (SourceID-sorted) UpdateList.  They come back ascending -- the
+// reference returned numpy argpartition order, and its only consumer,
+// checkIfAccepted, tests membership.  On any engine error every update is
+// rejected (empty list), which is what a failing Python call led to.
+func (krumval *KRUMValidator) getTopKRUMIndex(deltas [][]float64) []int {
+	n := len(deltas)
+	if n == 0 || bkCtx == nil {
+		return []int{}
+	}
+	d := len(deltas[0])
+	f := int(krumval.NumAdversaries * float64(n))
+	if C.bk_check_args(C.int64_t(n), C.int64_t(d), C.int64_t(f)) != C.BK_OK {
+		outLog.Printf("Krum: %s", C.GoString(C.bk_last_error()))
+		return []int{}
+	}
+	need := int64(n) * int64(d) * 8
+	if need > bkStageLen {
+		if bkStage != nil {
+			C.bk_stage_free(bkCtx, bkStage)
+		}
+		var p unsafe.Pointer
+		if C.bk_stage_alloc(bkCtx, C.int64_t(need), &p) != C.BK_OK {
+			outLog.Printf("Krum: %s", C.GoString(C.bk_last_error()))
+			bkStage, bkStageLen = nil, 0
+			return []int{}
+		}
+		bkStage, bkStageLen = p, need
+	}
+	// pack [][]float64 rows into the pinned C buffer (row-major n x d)
+	stage := unsafe.Slice((*float64)(bkStage), n*d)
+	for i := 0; i < n; i++ {
+		if len(deltas[i]) != d {
+			outLog.Printf("Krum: ragged update %d (%d != %d)", i, len(deltas[i]), d)
+			return []int{}
+		}
+		copy(stage[i*d:(i+1)*d], deltas[i])
+	}
+	m := n - f
+	sel := make([]C.int64_t, m)
+	var mOut C.int64_t
+	st := C.bk_multikrum(bkCtx, bkStage, C.BK_HOST_PINNED, C.BK_F64, C.int64_t(n), C.int64_t(d),
+		C.int64_t(d), C.int64_t(f), (*C.int64_t)(unsafe.Pointer(&sel[0])), &mOut, nil, nil)
+	if st != C.BK_OK {
+		outLog.Printf("Krum failed (%d): %s", int(st), C.GoString(C.bk_last_error()))
+		return []int{}
+	}
+	out := make([]int, int(mOut))
+	for i := range out {
+		out[i] = int(sel[i])
+	}
+	return out
+}
