@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--deterministic", action="store_true",
                     help="multi-GPU: all-gather + fixed-order sum instead of all-reduce")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the sharded path + RCCL communicator even at 1 rank")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,8 +124,10 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
-        tdist.init_process_group("nccl", device_id=dev)
+    sharded = world > 1 or a.sharded
+    if sharded:
+        if not tdist.is_initialized() and "MASTER_ADDR" in os.environ:
+            tdist.init_process_group("nccl", device_id=dev)
 
     w = WORKLOADS[a.workload]
     n, d, f = w["n"], w["d"], w["f"]
@@ -135,8 +139,11 @@ def main():
 
     eng = Engine(local_rank)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    if world > 1:
-        bootstrap_rccl(eng, rank, world, torch_broadcast_bytes)
+    if sharded:
+        if tdist.is_initialized():
+            bootstrap_rccl(eng, rank, world, torch_broadcast_bytes)
+        else:
+            bootstrap_rccl(eng, 0, 1, lambda b, src: b)
         eng.comm_set_mode(a.deterministic)
 
     X = torch.empty((n, max(dl, 1)), dtype=tdt, device=dev)
@@ -147,7 +154,7 @@ def main():
     mean = torch.empty(max(dl, 1), dtype=torch.float64, device=dev)
 
     def step():
-        if world == 1:
+        if not sharded:
             eng.multikrum_device_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f, sel.data_ptr(),
                                      scores.data_ptr(), mean.data_ptr())
         else:
@@ -207,7 +214,8 @@ def main():
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": w["dtype"],
         "data": "synthetic (repo SplitMix64 spec, generated on device; DESIGN.md)",
         "config": {"workload": a.workload, "n": n, "d": d, "f": f, "m": m,
-                   "parallelism": "d-shard x%d + RCCL all-reduce" % world if world > 1 else "1 GPU",
+                   "parallelism": ("d-shard x%d + RCCL %s" % (world, "all-gather" if a.deterministic else "all-reduce"))
+                   if sharded else "1 GPU",
                    "d_local": dl},
         "roofline": roof,
         "kernels_ms_avg": {k: round(v["avg_ms"], 5) for k, v in kt.items()},
@@ -245,7 +253,7 @@ def main():
 
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if tdist.is_initialized():
         tdist.barrier()
         tdist.destroy_process_group()
     eng.close()

@@ -200,3 +200,29 @@ def test_timing_api(engine):
     engine.timing_enable(False)
     for k in ("k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean"):
         assert t[k]["count"] == 3 and t[k]["avg_ms"] > 0
+
+
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_rccl_exchange_single_rank(engine, deterministic):
+    """The sharded entry with a real RCCL communicator (1 rank on this box):
+    the all-reduce / all-gather + fixed-order sum must leave the result
+    bitwise unchanged.  N > 1 runs are the driver's 8-GPU bench."""
+    from biscotti_amd.krum import Engine, comm_unique_id
+    e2 = Engine(0)
+    e2.set_stream(torch.cuda.current_stream().cuda_stream)
+    e2.comm_init(1, 0, comm_unique_id())
+    e2.comm_set_mode(deterministic)
+    n, d, f = 300, 70001, 90
+    X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 13, 90)
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    sc = torch.empty(n, dtype=torch.float64, device="cuda")
+    mean = torch.empty(d, dtype=torch.float64, device="cuda")
+    e2.multikrum_sharded_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr(),
+                             sc.data_ptr(), mean.data_ptr())
+    e2.synchronize()
+    fsel, fsc, fmean = _dev_run(engine, X, f)
+    assert np.array_equal(sel.cpu().numpy(), fsel)
+    assert np.array_equal(sc.cpu().numpy(), fsc)
+    assert np.array_equal(mean.cpu().numpy(), fmean)
+    e2.close()
