@@ -1,0 +1,84 @@
+"""Summarise a tools/profile.sh run into profiles/: per-kernel trace stats and
+PMC-derived HBM traffic per launch, corrected as MI355X_MICROARCH.md §HBM says:
+FETCH_SIZE (KiB) counts HALF the bytes of wide (16 B/lane) coalesced reads --
+global_load_dwordx4 and global_load_lds_dwordx4 alike -- so it is doubled for
+the kernels that read that way (k_gram3, k_mean); WRITE_SIZE is exact for
+16-B-per-lane stores and uncalibrated for narrower ones (noted, not scaled).
+
+    python tools/pmc_summary.py gpurun_out/prof_<tag> <workload> <out-prefix>
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+WIDE_READS = ("k_gram3", "k_mean", "k_gram<")
+
+
+def short(name):
+    s = name.replace("void ", "")
+    return s.split("(")[0].replace("bk::", "")
+
+
+def load_pmc(d):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for sub in sorted(os.listdir(d)):
+        p = os.path.join(d, sub, "run_counter_collection.csv")
+        if not sub.startswith("pmc") or not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
+
+
+def main():
+    prof, workload, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    stats = list(csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv"))))
+    pmc = load_pmc(prof)
+    res = {}
+    lines = ["# rocprofv3 summary: %s (%s)" % (workload, os.path.basename(prof)), "",
+             "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
+    for r in stats:
+        k = short(r["Name"])
+        lines.append("| %s | %s | %.1f | %.2f |" % (k, r["Calls"], float(r["AverageNs"]) / 1e3,
+                                                   float(r["Percentage"])))
+        res.setdefault(k, {})["avg_ms_rocprof"] = float(r["AverageNs"]) / 1e6
+    lines += ["", "| kernel | FETCH_SIZE KiB | read bytes (corrected) | WRITE_SIZE KiB | "
+              "HBM bytes/launch | TCC hit % | MFMA busy % | eff. clock GHz |",
+              "|---|---|---|---|---|---|---|---|"]
+    for k, c in sorted(pmc.items()):
+        if "FETCH_SIZE" not in c:
+            continue
+        fetch = c["FETCH_SIZE"] * 1024.0
+        corr = 2.0 if any(w in k for w in WIDE_READS) else 1.0
+        rd = fetch * corr
+        wr = c.get("WRITE_SIZE", 0.0) * 1024.0
+        hit = c.get("TCC_HIT_sum", 0.0)
+        miss = c.get("TCC_MISS_sum", 0.0)
+        hr = 100.0 * hit / (hit + miss) if hit + miss else float("nan")
+        busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        gui = c.get("GRBM_GUI_ACTIVE", 0.0)
+        avg = res.get(k, {}).get("avg_ms_rocprof")
+        clk = (gui / 8.0) / (avg * 1e-3) / 1e9 if gui and avg else float("nan")
+        simd_cycles = gui / 8.0 * 1024 if gui else 0
+        mb = 100.0 * busy / simd_cycles if simd_cycles else float("nan")
+        res.setdefault(k, {}).update(fetch_kib=c["FETCH_SIZE"], read_bytes_corrected=rd,
+                                     write_bytes=wr, hbm_bytes_per_launch=rd + wr,
+                                     tcc_hit_pct=hr, mfma_busy_pct=mb, clock_ghz=clk,
+                                     fetch_correction=corr)
+        lines.append("| %s | %.0f | %.3g | %.0f | %.3g | %.1f | %.1f | %.2f |" % (
+            k, c["FETCH_SIZE"], rd, c.get("WRITE_SIZE", 0.0), rd + wr, hr, mb, clk))
+    lines += ["", "FETCH_SIZE doubled (x2) for wide 16-B/lane reads per MI355X_MICROARCH.md §HBM;",
+              "WRITE_SIZE as reported.  MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)."]
+    k1 = next((k for k in res if k.startswith("k_gram")), None)
+    out_json = {"workload": workload, "source": prof, "kernels": res}
+    if k1:
+        out_json["k_gram"] = res[k1]
+    json.dump(out_json, open(out + ".json", "w"), indent=1)
+    open(out + ".md", "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
