@@ -1,0 +1,91 @@
+"""A/B two (or more) builds of libbk.so in ONE process on ONE GPU.
+
+Boxes differ by several percent, so kernel changes are compared by loading
+each build side by side (RTLD_LOCAL, separate code objects) and timing K1
+interleaved on the same device buffer:
+
+    python tools/ab_libs.py base=/path/libbk_base.so new=biscotti_amd/libbk.so \
+        nosum=biscotti_amd/libbk.so,BK_CSUM=0
+
+A ",KEY=VAL" suffix sets that env var while the build's context is created
+(the context reads BK_* knobs at bk_create).  Env: N, D, REPS.
+"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from biscotti_amd import _lib  # noqa: E402
+
+
+def load(spec):
+    path, *kv = spec.split(",")
+    env = dict(x.split("=", 1) for x in kv)
+    lib = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
+    for name, (res, args) in _lib.SIGNATURES.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+    ctx = ctypes.c_void_p()
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    st = lib.bk_create(ctypes.byref(ctx), 0)
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k)
+        else:
+            os.environ[k] = v
+    if st != 0:
+        raise RuntimeError("%s: bk_create %d %s" % (path, st, lib.bk_last_error()))
+    return lib, ctx
+
+
+def kgram_ms(lib, ctx, X, n, d, ld, U, reps=3):
+    lib.bk_gram_upper_device(ctx, X, _lib.BK_F64, n, d, ld, U)
+    lib.bk_synchronize(ctx)
+    lib.bk_timing_enable(ctx, 1)
+    for _ in range(reps):
+        st = lib.bk_gram_upper_device(ctx, X, _lib.BK_F64, n, d, ld, U)
+        assert st == 0, lib.bk_last_error()
+    lib.bk_synchronize(ctx)
+    ms, cnt = ctypes.c_double(), ctypes.c_int64()
+    lib.bk_timing_read(ctx, 0, ctypes.byref(ms), ctypes.byref(cnt))
+    lib.bk_timing_enable(ctx, 0)
+    return ms.value / max(cnt.value, 1)
+
+
+def main():
+    n, d = int(os.environ.get("N", 512)), int(os.environ.get("D", 1 << 20))
+    reps = int(os.environ.get("REPS", 8))
+    builds = []
+    for a in sys.argv[1:]:
+        label, path = a.split("=", 1)
+        builds.append((label,) + load(path))
+    X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    lib0, ctx0 = builds[0][1], builds[0][2]
+    lib0.bk_synth_fill_device(ctx0, X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 1, n // 3,
+                              0.01, 0.05, 1e-3, 0)
+    lib0.bk_synchronize(ctx0)
+    ue = int(lib0.bk_upper_elems(n))
+    Us = {}
+    for label, lib, ctx in builds:
+        Us[label] = torch.empty(ue, dtype=torch.float64, device="cuda")
+    res = {b[0]: [] for b in builds}
+    for _ in range(reps):
+        for label, lib, ctx in builds:
+            res[label].append(kgram_ms(lib, ctx, X.data_ptr(), n, d, d, Us[label].data_ptr()))
+    torch.cuda.synchronize()
+    ref = Us[builds[0][0]]
+    flops = n * (n + 1) * d
+    for label, v in res.items():
+        v = sorted(v)
+        same = bool(torch.equal(Us[label], ref))
+        print("%-8s n=%d d=%d k_gram median %.3f ms min %.3f ms (%.1f TF/s)  upper==%s: %s" %
+              (label, n, d, v[len(v) // 2], v[0], flops / (v[len(v) // 2] * 1e-3) / 1e12,
+               builds[0][0], same), flush=True)
+
+
+if __name__ == "__main__":
+    main()
