@@ -43,15 +43,16 @@ def needs_build():
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
-def build(force=False, verbose=True, extra=()):
-    if not force and not needs_build():
+def build(force=False, verbose=True, extra=(), out=LIB):
+    """extra/out: debug variants (e.g. -DBK_K1_PROBE into tools/ab/), never the product"""
+    if not force and out == LIB and not needs_build():
         return LIB
-    cmd = [HIPCC] + FLAGS + list(extra) + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB + ".tmp"] + LIBS
+    cmd = [HIPCC] + FLAGS + list(extra) + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out + ".tmp"] + LIBS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -73,7 +73,7 @@ struct bk_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace (grow-only)
-    DevBuf part, U, Ug, G, diag, scores, mask, sel, X, mean, perm;
+    DevBuf part, U, Ug, G, diag, scores, mask, sel, X, mean, perm, trace;
     // host-side pinned allocations handed out by bk_stage_alloc
     std::vector<void *> staged;
     // timing
@@ -265,10 +265,27 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
         CHK(ensure(c->part, (size_t)p3->nwg * 16 * 4096 * sizeof(double)));
         double *part = (double *)c->part.p;
         const Plan3 &P3 = *p3;
+        long long *trace = nullptr;
+        const char *tfile = getenv("BK_TRACE_FILE");  // debug: per-workgroup timeline
+        if (tfile) {
+            CHK(ensure(c->trace, (size_t)P3.nwg * 24 * sizeof(long long)));
+            HIPCHK(hipMemsetAsync(c->trace.p, 0, (size_t)P3.nwg * 24 * sizeof(long long), c->stream));
+            trace = (long long *)c->trace.p;
+        }
         CHK(timed(c, BK_K_GRAM, [&] {
             return launch_gram3((const double *)dX, ld, (int)n, d, P3, part, c->stream,
-                                c->gram_mode);
+                                c->gram_mode, trace);
         }));
+        if (tfile) {
+            std::vector<long long> h((size_t)P3.nwg * 24);
+            HIPCHK(hipMemcpyAsync(h.data(), trace, h.size() * sizeof(long long),
+                                  hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (FILE *fp = fopen(tfile, "ab")) {
+                fwrite(h.data(), sizeof(long long), h.size(), fp);
+                fclose(fp);
+            }
+        }
         CHK(timed(c, BK_K_REDUCE, [&] { return launch_reduce3(part, P3, U, c->stream); }));
         return BK_OK;
     }
@@ -397,7 +414,7 @@ void bk_destroy(bk_ctx *c) {
         DeviceGuard dg(c->device);
         (void)hipStreamSynchronize(c->stream);
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->G,    &c->diag, &c->scores,
-                          &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm};
+                          &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace};
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
         for (void *p : c->staged) (void)hipHostFree(p);

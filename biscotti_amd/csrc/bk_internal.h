@@ -61,7 +61,7 @@ struct Plan3Host {
 Plan3Host build_plan3(int n, int64_t d, int num_cu);
 
 hipError_t launch_gram3(const double *X, int64_t ld, int n, int64_t d, const Plan3 &pl,
-                        double *part, hipStream_t st, int mode = 0);
+                        double *part, hipStream_t st, int mode = 0, long long *trace = nullptr);
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st);
 hipError_t configure_kernels();
 hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan &pl,

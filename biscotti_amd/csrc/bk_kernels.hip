@@ -341,10 +341,17 @@ __device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const d2v (&a)[4], con
 // of each SIMD has MFMAs ready while its partner waits for its LDS reads.  The
 // accumulation order (block by block, column by column) is unchanged, so the
 // result is bitwise identical to the unstaggered schedule.
+// BK_K1_PROBE (debug builds only): shader cycles spent in the vmcnt wait and
+// in the barrier, per wave, reported through the BK_TRACE_FILE timeline
+#ifdef BK_K1_PROBE
+#define G3_PROBE(v) const long long v = (long long)__builtin_readcyclecounter()
+#else
+#define G3_PROBE(v) const long long v = 0
+#endif
 template <int KIND, int MODE, bool STAG>
 __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld, int n, int nfull,
                                         int64_t d, const GroupDesc &G, const int *wd, char *lds,
-                                        int wave, int lane, double *out) {
+                                        int wave, int lane, double *out, long long (&probe)[2]) {
     const int rr = lane & 15, g = lane >> 4;
     int blk[G3_MAXB];
 #pragma unroll
@@ -405,8 +412,13 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
     int buf = 0;
     for (int t = 0; t < nk; ++t) {
         const int ahead = min(nk - t - 1, G3_STAGES - 2);  // stages issued after t
+        G3_PROBE(p0);
         g3_wait(MODE == 2 ? 0 : ahead * c);
+        G3_PROBE(p1);
         g3_barrier();
+        G3_PROBE(p2);
+        probe[0] += p1 - p0;
+        probe[1] += p2 - p1;
         const char *ls = lds + buf * G3_STAGE;
         const int nbuf = buf == 0 ? G3_STAGES - 1 : buf - 1;  // (t + STAGES - 1) % STAGES
         const bool more = t + G3_STAGES - 1 < nk && MODE != 2;
@@ -514,22 +526,54 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const double *__restrict__ X, 
                                                   int nfull, int64_t d,
                                                   const GroupDesc *__restrict__ groups,
                                                   const int *__restrict__ wgtab,
-                                                  double *__restrict__ part) {
+                                                  double *__restrict__ part,
+                                                  long long *__restrict__ trace) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int *wd = wgtab + 5 * blockIdx.x;
+    // debug timeline (BK_TRACE_FILE): per workgroup 100 MHz start/end, shader
+    // clock start/end, HW_ID, XCC_ID
+    long long t_rt0 = 0, t_mt0 = 0;
+    if (trace && threadIdx.x == 0) {
+        t_rt0 = (long long)__builtin_amdgcn_s_memrealtime();
+        t_mt0 = (long long)__builtin_amdgcn_s_memtime();
+    }
     const GroupDesc &G = groups[wd[0]];
     double *out = part + ((int64_t)blockIdx.x * 16 + wave * 2) * 4096;
+    long long probe[2] = {0, 0};
     switch (G.task[wave][0]) {
     case T_OFF:
         if (wave >= 4 && G3_STAGGER)
-            g3_wave<T_OFF, MODE, true>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out);
+            g3_wave<T_OFF, MODE, true>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         else
-            g3_wave<T_OFF, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out);
+            g3_wave<T_OFF, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         break;
-    case T_PAIR: g3_wave<T_PAIR, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out); break;
-    case T_DIAG1: g3_wave<T_DIAG1, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out); break;
-    default: g3_wave<T_NONE, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out); break;
+    case T_PAIR: g3_wave<T_PAIR, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+    case T_DIAG1: g3_wave<T_DIAG1, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+    default: g3_wave<T_NONE, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+    }
+    if (trace) {
+#ifdef BK_K1_PROBE
+        if (lane == 0) {
+            trace[24 * blockIdx.x + 8 + wave] = probe[0];
+            trace[24 * blockIdx.x + 16 + wave] = probe[1];
+        }
+#endif
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            long long *tr = trace + 24 * blockIdx.x;
+            tr[0] = t_rt0;
+            tr[1] = (long long)__builtin_amdgcn_s_memrealtime();
+            tr[2] = t_mt0;
+            tr[3] = (long long)__builtin_amdgcn_s_memtime();
+            tr[4] = hw;
+            tr[5] = xcc;
+            tr[6] = wd[0] | ((long long)G.cost << 32);
+            tr[7] = wd[1] < wd[3] ? (wd[3] - 1 - wd[1]) / wd[2] + 1 : 0;
+        }
     }
 }
 
@@ -885,17 +929,17 @@ hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, i
 }
 
 hipError_t launch_gram3(const double *X, int64_t ld, int n, int64_t d, const Plan3 &pl,
-                        double *part, hipStream_t st, int mode) {
+                        double *part, hipStream_t st, int mode, long long *trace) {
     // mode != 0: timing-only ablations (1: no MFMA, 2: no global loads) -- wrong results
     if (mode == 1)
         hipLaunchKernelGGL(k_gram3<1>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
-                           pl.nfull, d, pl.d_groups, pl.d_wg, part);
+                           pl.nfull, d, pl.d_groups, pl.d_wg, part, trace);
     else if (mode == 2)
         hipLaunchKernelGGL(k_gram3<2>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
-                           pl.nfull, d, pl.d_groups, pl.d_wg, part);
+                           pl.nfull, d, pl.d_groups, pl.d_wg, part, trace);
     else
         hipLaunchKernelGGL(k_gram3<0>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
-                           pl.nfull, d, pl.d_groups, pl.d_wg, part);
+                           pl.nfull, d, pl.d_groups, pl.d_wg, part, trace);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdint>
+#include <cstdlib>
 #include <functional>
 #include <queue>
 #include <vector>
@@ -21,6 +22,16 @@ namespace bk {
 namespace {
 
 constexpr int COST_OFF = 16, COST_PAIR = 20, COST_DIAG1 = 10;
+// measured on MI355X (tools/trace_gram.py): a k-block of a group costs about
+// 256 * cost + 191 * nb shader cycles -- each staged row-block adds ~0.75 cost
+// units of memory stall.  Apportioning by this (not by MFMA cost alone) keeps
+// the column fronts of all groups on an XCD together, so the row-blocks they
+// share are re-read from L2 instead of HBM.
+double eff_cost(const GroupDesc &g) {
+    const char *v = getenv("BK_PLAN_NB_COST");
+    const double a = v ? atof(v) : 0.75;
+    return g.cost + a * g.nb;
+}
 
 struct Task {
     int kind;
@@ -182,33 +193,40 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu) {
     const int per_xcd = std::max(1, num_cu / NX);
     std::vector<int64_t> K(NX + 1);
     for (int x = 0; x <= NX; ++x) K[x] = (int64_t)nfull * x / NX;
-    double csum = 0;
-    for (auto &g : G) csum += g.cost;
-    const double wg_overhead = 64.0 * 24.0;  // prologue + slab write, in cost * k-block units
+    // prologue (ring fill at loaded latency) + partial-slab write + reduce share,
+    // in cost units (256 shader cycles): ~10 us per workgroup
+    const char *ev = getenv("BK_PLAN_WGOH");
+    const double wg_overhead = ev ? atof(ev) : 100.0;
+    const char *er = getenv("BK_PLAN_ROUNDS");
+    const int force_rounds = er ? atoi(er) : 0;
     double best = 1e300;
     std::vector<int> bestQ(ng, 1);
     for (int rounds = 1; rounds <= 16; rounds *= 2) {
+        if (force_rounds && rounds != force_rounds) continue;
         const double slots_total = (double)rounds * per_xcd;
         if (ng > slots_total * 4) continue;
-        // largest-remainder apportionment of the XCD's slots, Q_g >= 1
-        std::vector<int> Q(ng);
-        std::vector<std::pair<double, int>> rem;
-        int used = 0;
-        for (int g = 0; g < ng; ++g) {
-            const double want = slots_total * G[g].cost / csum;
-            Q[g] = std::max(1, (int)want);
-            used += Q[g];
-            rem.push_back({want - (int)want, g});
+        // min-max apportionment of the XCD's slots (Q_g >= 1): repeatedly give a
+        // slot to the group with the largest eff_g / Q_g.  Equal eff_g / Q_g both
+        // balances the workgroups and makes every group's column front advance
+        // at the same speed (shared row-blocks stay in L2).
+        std::vector<int> Q(ng, 1);
+        {
+            std::priority_queue<std::pair<double, int>> pq;
+            for (int g = 0; g < ng; ++g) pq.push({eff_cost(G[g]), g});
+            for (int used = ng; used < (int)slots_total; ++used) {
+                const int g = pq.top().second;
+                pq.pop();
+                Q[g]++;
+                pq.push({eff_cost(G[g]) / Q[g], g});
+            }
         }
-        std::sort(rem.begin(), rem.end(), [](auto &a, auto &b) { return a.first > b.first; });
-        for (size_t i = 0; i < rem.size() && used < (int)slots_total; ++i, ++used) Q[rem[i].second]++;
         // list-schedule one XCD's workgroups (largest first) on per_xcd slots
         std::vector<double> jobs;
         const int64_t R = K[1] - K[0];
         for (int g = 0; g < ng; ++g)
             for (int q = 0; q < Q[g]; ++q) {
                 const int64_t nk = q < R ? (R - 1 - q) / Q[g] + 1 : 0;
-                jobs.push_back((double)nk * G[g].cost + wg_overhead);
+                jobs.push_back((double)nk * eff_cost(G[g]) + wg_overhead);
             }
         std::priority_queue<double, std::vector<double>, std::greater<double>> slots;
         for (int i = 0; i < per_xcd; ++i) slots.push(0.0);

@@ -39,7 +39,24 @@ def load(spec):
             os.environ[k] = v
     if st != 0:
         raise RuntimeError("%s: bk_create %d %s" % (path, st, lib.bk_last_error()))
-    return lib, ctx
+    return lib, ctx, env
+
+
+class _env:
+    """the build's env knobs also apply while it runs (plans are built lazily)"""
+    def __init__(self, env):
+        self.env = env
+
+    def __enter__(self):
+        self.saved = {k: os.environ.get(k) for k in self.env}
+        os.environ.update(self.env)
+
+    def __exit__(self, *a):
+        for k, v in self.saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
 
 
 def kgram_ms(lib, ctx, X, n, d, ld, U, reps=3):
@@ -70,12 +87,13 @@ def main():
     lib0.bk_synchronize(ctx0)
     ue = int(lib0.bk_upper_elems(n))
     Us = {}
-    for label, lib, ctx in builds:
+    for label, lib, ctx, env in builds:
         Us[label] = torch.empty(ue, dtype=torch.float64, device="cuda")
     res = {b[0]: [] for b in builds}
     for _ in range(reps):
-        for label, lib, ctx in builds:
-            res[label].append(kgram_ms(lib, ctx, X.data_ptr(), n, d, d, Us[label].data_ptr()))
+        for label, lib, ctx, env in builds:
+            with _env(env):
+                res[label].append(kgram_ms(lib, ctx, X.data_ptr(), n, d, d, Us[label].data_ptr()))
     torch.cuda.synchronize()
     ref = Us[builds[0][0]]
     flops = n * (n + 1) * d
