@@ -47,9 +47,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(w, target_s=12.0):
+def cpu_baseline(w, target_s=10.0, target_1core_s=6.0):
     """Time the oracle (C/OpenMP restatement of the reference's numpy krum,
-    oracle/krum_oracle.c) on a bounded column sample of the same batch."""
+    oracle/krum_oracle.c) on a bounded column sample of the same batch, on all
+    the host threads OpenMP is given and on 1 core."""
     from oracle import oracle as O
     n, d, f = w["n"], w["d"], w["f"]
     dt = np.float32 if w["dtype"] == "f32" else np.float64
@@ -62,18 +63,82 @@ def cpu_baseline(w, target_s=12.0):
         O.krum(X, f)
         return time.perf_counter() - t0
 
-    ds = min(d, 32768)
-    t = run(ds)
-    if t < target_s / 4 and ds < d:
-        ds2 = int(min(d, ds * max(1.0, target_s / max(t, 1e-3))))
-        ds2 = max(8, ds2 // 8 * 8)
-        if ds2 > ds:
-            ds, t = ds2, run(ds2)
-    return {"value": round(n * ds * es / t / 1e9, 4), "unit": "GB/s", "cores": O.num_threads(),
-            "kind": "port",
-            "sample": "oracle/krum_oracle.c (OpenMP) full Multi-Krum (Gram, sort, select, mean) "
-                      "on the first %d of %d columns of the same %dx%d batch, %.2f s" %
-                      (ds, d, n, d, t)}
+    def sized(ds, target):
+        t = run(ds)
+        if t < target / 4 and ds < d:
+            ds2 = int(min(d, ds * max(1.0, target / max(t, 1e-3))))
+            ds2 = max(8, ds2 // 8 * 8)
+            if ds2 > ds:
+                ds, t = ds2, run(ds2)
+        return ds, t
+
+    cores = O.num_threads()
+    ds, t = sized(min(d, 32768), target_s)
+    out = {"value": round(n * ds * es / t / 1e9, 4), "unit": "GB/s", "cores": cores,
+           "kind": "port",
+           "sample": "oracle/krum_oracle.c (OpenMP, %d threads) full Multi-Krum (Gram, sort, "
+                     "select, mean) on the first %d of %d columns of the same %dx%d batch, %.2f s"
+                     % (cores, ds, d, n, d, t)}
+    O.set_threads(1)
+    try:
+        ds1, t1 = sized(min(d, 2048), target_1core_s)
+    finally:
+        O.set_threads(cores)
+    out["value_1core"] = round(n * ds1 * es / t1 / 1e9, 4)
+    out["sample_1core"] = "same, 1 thread, first %d columns, %.2f s" % (ds1, t1)
+    return out
+
+
+def next_rows(eng, X, n, d, sel, m, steps=5):
+    """SURVEY.md §8(f) rows 2-3 on the same device-resident batch (HBM-bound):
+    block aggregation of the m selected rows into GlobalW (K4'), the
+    secure-path quantised int64 sum (K5), and noise application to 128 of the
+    updates with k = 2 noise vectors each (K6).  Algorithmic bytes:
+    aggregate m*d*8 + 2*d*8; qsum m*d*8 + 2*d*8; noise rows*d*8*(k+2)."""
+    import torch
+    from biscotti_amd import _lib
+    dev = X.device
+    g = torch.zeros(d, dtype=torch.float64, device=dev)
+    s = torch.empty(d, dtype=torch.int64, device=dev)
+    sf = torch.empty(d, dtype=torch.float64, device=dev)
+    rows, k = 128, 2
+    noise = torch.empty((rows * k, d), dtype=torch.float64, device=dev)
+    eng.synth_fill_ptr(noise.data_ptr(), _lib.BK_F64, rows * k, d, d, 0, d, 7, 0, 0.0, 0.0, 1e-3)
+    out = torch.empty((rows, d), dtype=torch.float64, device=dev)
+    runs = {
+        "k_aggregate": (lambda: eng.aggregate_device_ptr(X.data_ptr(), _lib.BK_F64, n, d,
+                                                         X.stride(0), sel.data_ptr(), m,
+                                                         g.data_ptr()),
+                        m * d * 8 + 2 * d * 8,
+                        "GlobalW += sum of the %d selected rows (honest.go:360-375)" % m),
+        "k_qsum": (lambda: eng.quantized_sum_ptr(X.data_ptr(), _lib.BK_F64, n, d, X.stride(0),
+                                                 sel.data_ptr(), m, 4, s.data_ptr(),
+                                                 sf.data_ptr()),
+                   m * d * 8 + 2 * d * 8,
+                   "int64(x*1e4) summed over the %d selected rows (kyber.go:698-757)" % m),
+        "k_noise": (lambda: eng.noise_apply_ptr(X.data_ptr(), rows, d, X.stride(0),
+                                                noise.data_ptr(), k, d, out.data_ptr(), d),
+                    rows * d * 8 * (k + 2),
+                    "NoisedDelta = Delta + mean of %d noise vectors, %d updates "
+                    "(main.go:1524-1537, 1606-1653)" % (k, rows)),
+    }
+    res = {}
+    for name, (fn, nbytes, what) in runs.items():
+        fn()
+        torch.cuda.synchronize()
+        eng.timing_enable(True)
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        t = eng.timing_read().get(name)
+        eng.timing_enable(False)
+        ms = t["avg_ms"]
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        res[name] = {"what": what, "ms": round(ms, 4), "bytes": nbytes, "GB_per_s": round(gbs, 1),
+                     "roofline": {"bound": "hbm", "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                  "frac": round(gbs / PEAK_HBM_GBS, 4)}}
+    del noise, out
+    return res
 
 
 def golden_check(name, sel_host, mean_local, c0, dl):
@@ -103,6 +168,8 @@ def main():
     ap.add_argument("--workload", default=DEFAULT_WORKLOAD, choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-next-rows", action="store_true",
+                    help="skip the §8(f) aggregation / quantised-sum / noise measurements")
     ap.add_argument("--deterministic", action="store_true",
                     help="multi-GPU: all-gather + fixed-order sum instead of all-reduce")
     ap.add_argument("--sharded", action="store_true",
@@ -190,6 +257,41 @@ def main():
 
     parity = golden_check(a.workload, sel.cpu().numpy(), mean[:dl].cpu().numpy(), c0, dl)
 
+    variants = {}
+    if a.workload == "D_512x1M_f153":
+        # the reference's own clip rule, f = int(0.5 n) (krum.go:110), on the same batch
+        f2 = n // 2
+        sel2 = torch.empty(n - f2, dtype=torch.int64, device=dev)
+
+        def step2():
+            if not sharded:
+                eng.multikrum_device_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f2,
+                                         sel2.data_ptr(), scores.data_ptr(), mean.data_ptr())
+            else:
+                eng.multikrum_sharded_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f2,
+                                          sel2.data_ptr(), scores.data_ptr(), mean.data_ptr())
+        step2()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        k2 = max(3, a.steps // 4)
+        t0 = time.perf_counter()
+        for _ in range(k2):
+            step2()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        e2 = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([e2], dtype=torch.float64, device=dev)
+            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+            e2 = float(tt.item())
+        variants["D_512x1M_f256"] = {
+            "f": f2, "m": n - f2, "steps": k2, "ms_per_step": round(e2 / k2 * 1e3, 4),
+            "value": round(n * d * es / (e2 / k2) / 1e9, 3),
+            "parity": golden_check("D_512x1M_f256", sel2.cpu().numpy(),
+                                   mean[:dl].cpu().numpy(), c0, dl)}
+
     # roofline of the dominant kernel (K1, fp64 MFMA): algorithmic flops per
     # launch = n(n+1) * d_local (symmetric Gram incl. diagonal)
     g = kt.get("k_gram", {"avg_ms": float("nan")})
@@ -221,6 +323,11 @@ def main():
         "kernels_ms_avg": {k: round(v["avg_ms"], 5) for k, v in kt.items()},
         "parity": parity,
     }
+    if variants:
+        out["variants"] = variants
+
+    if rank == 0 and world == 1 and not a.no_next_rows and w["dtype"] == "f64":
+        out["next_rows"] = next_rows(eng, X, n, d, sel, m)
 
     if rank == 0 and world == 1 and not a.no_e2e:
         # PCIe-inclusive rate: pinned host batch -> H2D -> Multi-Krum -> D2H of sel and mean

@@ -57,7 +57,8 @@ int fail(int code, const char *fmt, ...) {
 
 const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_expand", "k_scores",
                                             "k_rank",    "k_compact", "k_mean",   "allreduce",
-                                            "k_synth",   "h2d",       "d2h"};
+                                            "k_synth",   "h2d",       "d2h",
+                                            "k_aggregate", "k_qsum",  "k_noise"};
 
 struct DevBuf {
     void *p = nullptr;
@@ -73,7 +74,7 @@ struct bk_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace (grow-only)
-    DevBuf part, U, Ug, G, diag, scores, mask, sel, X, mean, perm, trace;
+    DevBuf part, U, Ug, G, diag, scores, mask, sel, X, mean, perm, trace, idx;
     // host-side pinned allocations handed out by bk_stage_alloc
     std::vector<void *> staged;
     // timing
@@ -398,6 +399,7 @@ int bk_create(bk_ctx **out, int device) {
         if (strcmp(v, "v1") == 0) c->gram_variant = 1;
     if (const char *v = getenv("BK_GRAM_MODE")) c->gram_mode = atoi(v);
     e = configure_kernels();
+    if (e == hipSuccess) e = configure_aggregate_kernels();
     if (e != hipSuccess) {
         (void)hipStreamDestroy(c->own);
         delete c;
@@ -414,7 +416,7 @@ void bk_destroy(bk_ctx *c) {
         DeviceGuard dg(c->device);
         (void)hipStreamSynchronize(c->stream);
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->G,    &c->diag, &c->scores,
-                          &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace};
+                          &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx};
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
         for (void *p : c->staged) (void)hipHostFree(p);
@@ -728,3 +730,109 @@ int bk_timing_read(bk_ctx *c, int kid, double *total_ms, int64_t *count) {
 }
 
 }  // extern "C"
+
+// ---- block aggregation, quantised sum, noise ------
+static int check_rows(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
+                      int64_t m) {
+    CHK(check_common(c, dX, dtype, n, d, ld));
+    if (m < 0) return fail(BK_EINVAL, "m=%lld < 0", (long long)m);
+    if (m > BK_MAX_N) return fail(BK_ENOTSUP, "m=%lld exceeds BK_MAX_N=%d", (long long)m, BK_MAX_N);
+    return BK_OK;
+}
+
+int bk_aggregate_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
+                        const int64_t *d_idx, int64_t m, double *d_global) {
+    CHK(check_rows(c, dX, dtype, n, d, ld, m));
+    if (!d_global || (m > 0 && !d_idx)) return fail(BK_EINVAL, "null d_idx / d_global");
+    if (m == 0) return BK_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    return timed(c, BK_K_AGGREGATE, [&] {
+        return launch_accumulate(dX, dtype, ld, d, d_idx, (int)m, d_global, c->num_cu, c->stream);
+    });
+}
+
+int bk_aggregate(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int64_t d, int64_t ld,
+                 const int64_t *idx, int64_t m, double *global) {
+    CHK(check_rows(c, X, dtype, n, d, ld, m));
+    if (!global || (m > 0 && !idx)) return fail(BK_EINVAL, "null idx / global");
+    if (where != BK_HOST && where != BK_HOST_PINNED && where != BK_DEVICE)
+        return fail(BK_EINVAL, "bad where=%d", where);
+    for (int64_t r = 0; r < m; ++r)
+        if (idx[r] < 0 || idx[r] >= n)
+            return fail(BK_EINVAL, "idx[%lld]=%lld out of [0,%lld)", (long long)r,
+                        (long long)idx[r], (long long)n);
+    if (m == 0) return BK_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    const size_t es = esize(dtype);
+    const void *dX = X;
+    int64_t dld = ld;
+    if (where != BK_DEVICE) {
+        // only the accepted rows cross PCIe: gather them (in idx order) into the stage
+        CHK(ensure(c->X, (size_t)m * d * es));
+        char *dst = (char *)c->X.p;
+        CHK(timed(c, BK_K_H2D, [&] {
+            hipError_t e = hipSuccess;
+            for (int64_t r = 0; r < m && e == hipSuccess; ++r)
+                e = hipMemcpyAsync(dst + (size_t)r * d * es, (const char *)X + (size_t)idx[r] * ld * es,
+                                   (size_t)d * es, hipMemcpyHostToDevice, c->stream);
+            return e;
+        }));
+        dX = dst;
+        dld = d;
+    }
+    CHK(ensure(c->idx, (size_t)m * sizeof(int64_t)));
+    CHK(ensure(c->mean, (size_t)d * sizeof(double)));
+    int64_t *didx = (int64_t *)c->idx.p;
+    double *dglob = (double *)c->mean.p;
+    std::vector<int64_t> hidx((size_t)m);
+    for (int64_t r = 0; r < m; ++r) hidx[r] = where != BK_DEVICE ? r : idx[r];
+    HIPCHK(hipMemcpyAsync(didx, hidx.data(), (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(dglob, global, (size_t)d * sizeof(double), hipMemcpyHostToDevice,
+                          c->stream));
+    CHK(timed(c, BK_K_AGGREGATE, [&] {
+        return launch_accumulate(dX, dtype, dld, d, didx, (int)m, dglob, c->num_cu, c->stream);
+    }));
+    CHK(timed(c, BK_K_D2H, [&] {
+        return hipMemcpyAsync(global, dglob, (size_t)d * sizeof(double), hipMemcpyDeviceToHost,
+                              c->stream);
+    }));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BK_OK;
+}
+
+int bk_quantized_sum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
+                            int64_t ld, const int64_t *d_idx, int64_t m, int precision,
+                            int64_t *d_sum, double *d_sum_float) {
+    CHK(check_rows(c, dX, dtype, n, d, ld, m));
+    if (!d_sum || (m > 0 && !d_idx)) return fail(BK_EINVAL, "null d_idx / d_sum");
+    if (precision < 0 || precision > 18)
+        return fail(BK_EINVAL, "precision=%d outside [0, 18]", precision);
+    double scale = 1.0;  // 10^p, exact for p <= 22 (what Go's math.Pow(10, p) returns)
+    for (int i = 0; i < precision; ++i) scale *= 10.0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    return timed(c, BK_K_QSUM, [&] {
+        return launch_qsum(dX, dtype, ld, d, d_idx, (int)m, scale, d_sum, d_sum_float, c->num_cu,
+                           c->stream);
+    });
+}
+
+int bk_noise_apply_device(bk_ctx *c, const double *d_delta, int64_t n, int64_t d, int64_t ld,
+                          const double *d_noise, int64_t k, int64_t noise_ld, double *d_out,
+                          int64_t out_ld) {
+    CHK(check_common(c, d_delta, BK_F64, n, d, ld));
+    if (!d_out || (k > 0 && !d_noise)) return fail(BK_EINVAL, "null d_noise / d_out");
+    if (k < 0) return fail(BK_EINVAL, "k=%lld < 0", (long long)k);
+    if (k > 0 && noise_ld < d) return fail(BK_EINVAL, "noise_ld=%lld < d", (long long)noise_ld);
+    if (out_ld < d) return fail(BK_EINVAL, "out_ld=%lld < d", (long long)out_ld);
+    if (d_out == d_delta && out_ld != ld) return fail(BK_EINVAL, "in-place needs out_ld == ld");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    return timed(c, BK_K_NOISE, [&] {
+        return launch_noise(d_delta, ld, n, d, d_noise, k, noise_ld, d_out, out_ld, c->num_cu,
+                            c->stream);
+    });
+}

@@ -76,6 +76,16 @@ hipError_t launch_rank(const double *scores, int n, int m, int *mask, hipStream_
 hipError_t launch_compact(const int *mask, int n, int64_t *sel, hipStream_t st);
 hipError_t launch_mean(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel, int m,
                        double *mean, int num_cu, hipStream_t st);
+// global[c] += X[idx[0]][c] + X[idx[1]][c] + ... (sequential, idx order)
+hipError_t launch_accumulate(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *idx,
+                             int m, double *global, int num_cu, hipStream_t st);
+// bk_aggregate.hip
+hipError_t launch_qsum(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *idx, int m,
+                       double scale, int64_t *sum, double *sumf, int num_cu, hipStream_t st);
+hipError_t launch_noise(const double *delta, int64_t ld, int64_t n, int64_t d, const double *noise,
+                        int64_t k, int64_t nld, double *out, int64_t old, int num_cu,
+                        hipStream_t st);
+hipError_t configure_aggregate_kernels();
 hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, int64_t c0,
                         const int64_t *perm, const SynthParams &P, hipStream_t st);
 

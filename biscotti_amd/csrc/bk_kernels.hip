@@ -11,6 +11,7 @@
 //   K3  k_rank      rank of each score (ties -> lower index, NaN last), mask
 //   K3b k_compact   mask -> ascending selected indices (argpartition set, :45)
 //   K4  k_mean      masked mean of the selected rows, fp64, ascending order (:51)
+//                   (ACCUM: the block aggregation GlobalW += sum, honest.go:361-375)
 //
 // Built with -ffp-contract=off: every non-MFMA add/mul rounds exactly as the
 // numpy reference evaluates it.
@@ -758,7 +759,10 @@ __global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, 
 // ---------------------------------------------------------------------------
 // K4: mean[c] = (sum over selected rows, ascending) / m      (:51, fp64)
 // ---------------------------------------------------------------------------
-template <typename T, bool VEC>
+// ACCUM = false: mean[c] = (sum over r in sel order of X[sel[r]][c]) / m   (K4)
+// ACCUM = true:  mean[c] = mean[c] + X[sel[0]][c] + X[sel[1]][c] + ...       (in sel
+//                order, sequential: the GlobalW update of honest.go:361-375)
+template <typename T, bool VEC, bool ACCUM = false>
 __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t ld, int64_t d,
                                               const int64_t *__restrict__ sel, int m,
                                               double *__restrict__ mean) {
@@ -772,6 +776,7 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
         const int64_t c = cp * 2;
         if (c + 1 < d) {
             d2v acc = {0.0, 0.0};
+            if constexpr (ACCUM) acc = d2v{mean[c], mean[c + 1]};
             int r = 0;
             for (; r + 8 <= m; r += 8) {
                 d2v v[8];
@@ -788,12 +793,17 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
                 acc.x += v.x;
                 acc.y += v.y;
             }
-            mean[c] = acc.x / dm;
-            mean[c + 1] = acc.y / dm;
+            if constexpr (ACCUM) {
+                mean[c] = acc.x;
+                mean[c + 1] = acc.y;
+            } else {
+                mean[c] = acc.x / dm;
+                mean[c + 1] = acc.y / dm;
+            }
         } else {
-            double acc = 0.0;
+            double acc = ACCUM ? mean[c] : 0.0;
             for (int r = 0; r < m; ++r) acc += (double)X[srow[r] + c];
-            mean[c] = acc / dm;
+            mean[c] = ACCUM ? acc : acc / dm;
         }
     }
 }
@@ -886,8 +896,23 @@ hipError_t launch_compact(const int *mask, int n, int64_t *sel, hipStream_t st) 
     return hipGetLastError();
 }
 
+template <bool ACCUM>
+static hipError_t launch_colsum(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel,
+                                int m, double *mean, int num_cu, hipStream_t st);
+
 hipError_t launch_mean(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel, int m,
                        double *mean, int num_cu, hipStream_t st) {
+    return launch_colsum<false>(X, dtype, ld, d, sel, m, mean, num_cu, st);
+}
+
+hipError_t launch_accumulate(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *idx,
+                             int m, double *global, int num_cu, hipStream_t st) {
+    return launch_colsum<true>(X, dtype, ld, d, idx, m, global, num_cu, st);
+}
+
+template <bool ACCUM>
+static hipError_t launch_colsum(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel,
+                                int m, double *mean, int num_cu, hipStream_t st) {
     const int64_t npair = (d + 1) / 2;
     int64_t blocks = (npair + 255) / 256;
     const int64_t cap = (int64_t)num_cu * 16;
@@ -899,17 +924,17 @@ hipError_t launch_mean(const void *X, int dtype, int64_t ld, int64_t d, const in
     dim3 grid((unsigned)blocks), block(256);
     if (dtype == 0) {
         if (vec)
-            hipLaunchKernelGGL((k_mean<double, true>), grid, block, lds, st, (const double *)X, ld, d,
+            hipLaunchKernelGGL((k_mean<double, true, ACCUM>), grid, block, lds, st, (const double *)X, ld, d,
                                sel, m, mean);
         else
-            hipLaunchKernelGGL((k_mean<double, false>), grid, block, lds, st, (const double *)X, ld,
+            hipLaunchKernelGGL((k_mean<double, false, ACCUM>), grid, block, lds, st, (const double *)X, ld,
                                d, sel, m, mean);
     } else {
         if (vec)
-            hipLaunchKernelGGL((k_mean<float, true>), grid, block, lds, st, (const float *)X, ld, d,
+            hipLaunchKernelGGL((k_mean<float, true, ACCUM>), grid, block, lds, st, (const float *)X, ld, d,
                                sel, m, mean);
         else
-            hipLaunchKernelGGL((k_mean<float, false>), grid, block, lds, st, (const float *)X, ld, d,
+            hipLaunchKernelGGL((k_mean<float, false, ACCUM>), grid, block, lds, st, (const float *)X, ld, d,
                                sel, m, mean);
     }
     return hipGetLastError();
@@ -962,17 +987,19 @@ hipError_t configure_kernels() {
     e = hipFuncSetAttribute((const void *)k_scores<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             131072);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void *)k_mean<double, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void *)k_mean<double, false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void *)k_mean<float, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void *)k_mean<float, false>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    // the masked column sums keep up to BK_MAX_N row offsets in LDS
+    for (const void *k : {(const void *)k_mean<double, true, false>,
+                          (const void *)k_mean<double, false, false>,
+                          (const void *)k_mean<float, true, false>,
+                          (const void *)k_mean<float, false, false>,
+                          (const void *)k_mean<double, true, true>,
+                          (const void *)k_mean<double, false, true>,
+                          (const void *)k_mean<float, true, true>,
+                          (const void *)k_mean<float, false, true>}) {
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace bk

@@ -98,6 +98,38 @@ class Engine:
         check(lib().bk_multikrum_sharded_device(self._ctx, _p(x_ptr), dtype, n, d_local, ld, f,
                                                 _p(sel_ptr), _p(scores_ptr), _p(mean_ptr)))
 
+    # ---- SURVEY §8(f) rows 2-3 (bk_aggregate*, bk_quantized_sum_device,
+    #      bk_noise_apply_device) --------------------------------------------
+    def aggregate(self, X, idx, global_w):
+        """global_w += X[idx[0]] + X[idx[1]] + ... in place (host arrays; bk_aggregate)."""
+        X = np.asarray(X)
+        if X.dtype not in (np.float64, np.float32):
+            X = X.astype(np.float64)
+        if X.strides[1] != X.itemsize or X.strides[0] % X.itemsize:
+            X = np.ascontiguousarray(X)
+        n, d = X.shape
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        if global_w.dtype != np.float64 or not global_w.flags.c_contiguous or global_w.shape != (d,):
+            raise ValueError("global_w must be a C-contiguous float64 vector of length d")
+        dt = _lib.BK_F32 if X.dtype == np.float32 else _lib.BK_F64
+        check(lib().bk_aggregate(self._ctx, X.ctypes.data, _lib.BK_HOST, dt, n, d,
+                                 X.strides[0] // X.itemsize, idx.ctypes.data, len(idx),
+                                 global_w.ctypes.data))
+        return global_w
+
+    def aggregate_device_ptr(self, x_ptr, dtype, n, d, ld, idx_ptr, m, global_ptr):
+        check(lib().bk_aggregate_device(self._ctx, _p(x_ptr), dtype, n, d, ld, _p(idx_ptr), m,
+                                        _p(global_ptr)))
+
+    def quantized_sum_ptr(self, x_ptr, dtype, n, d, ld, idx_ptr, m, precision, sum_ptr,
+                          sumf_ptr=None):
+        check(lib().bk_quantized_sum_device(self._ctx, _p(x_ptr), dtype, n, d, ld, _p(idx_ptr), m,
+                                            int(precision), _p(sum_ptr), _p(sumf_ptr)))
+
+    def noise_apply_ptr(self, delta_ptr, n, d, ld, noise_ptr, k, noise_ld, out_ptr, out_ld):
+        check(lib().bk_noise_apply_device(self._ctx, _p(delta_ptr), n, d, ld, _p(noise_ptr), k,
+                                          noise_ld, _p(out_ptr), out_ld))
+
     def gram_upper_ptr(self, x_ptr, dtype, n, d, ld, upper_ptr):
         check(lib().bk_gram_upper_device(self._ctx, _p(x_ptr), dtype, n, d, ld, _p(upper_ptr)))
 

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 1
+#define BK_ABI_VERSION 2
 
 typedef struct bk_ctx bk_ctx;
 
@@ -128,6 +128,47 @@ int bk_synth_fill_device(bk_ctx *ctx, void *dX, int dtype, int64_t n, int64_t d_
                          int64_t ld, int64_t c0, int64_t d_total, uint64_t seed, int64_t nbyz,
                          double mu_scale, double byz_scale, double sigma, int flags);
 
+/* ---- the steps either side of Multi-Krum --- */
+
+/* Block aggregation of the accepted updates -- replaces the update loop of
+ * Honest.createBlock, DistSys/honest.go:360-375 (pulledGradientM.Add per
+ * accepted update, in blockUpdates order):
+ *     for r = 0 .. m-1:  global[c] = global[c] + X[idx[r]][c]
+ * sequential fp64 adds in idx order, bit-identical to the Go loop.  idx lists
+ * the accepted rows in the caller's update order (duplicates allowed); m = 0
+ * leaves global unchanged.  The stake bookkeeping (+-STAKE_UNIT) stays above
+ * the boundary.  Device variant: d_idx entries must lie in [0, n) (not checked
+ * on the device); m <= BK_MAX_N. */
+int bk_aggregate_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
+                        const int64_t *d_idx, int64_t m, double *d_global);
+/* Host-buffer variant for the Go miner: X as in bk_multikrum (where), idx and
+ * global (in/out, d entries) in host memory; idx is range-checked (BK_EINVAL). */
+int bk_aggregate(bk_ctx *ctx, const void *X, int where, int dtype, int64_t n, int64_t d,
+                 int64_t ld, const int64_t *idx, int64_t m, double *global);
+
+/* Secure-aggregation quantised sum -- updateFloatToInt (DistSys/kyber.go:698-710)
+ * of each accepted update, summed as the miners' share aggregation does before
+ * recovery (honest.go:401-409, 442-502), and updateIntToFloat (kyber.go:745-757):
+ *     d_sum[c]       = sum_r int64(X[idx[r]][c] * 10^precision)   (int64, wrapping)
+ *     d_sum_float[c] = float64(d_sum[c]) / 10^precision           (nullable)
+ * int64(float64) follows Go on amd64: truncation toward zero, NaN and
+ * out-of-range values give INT64_MIN.  0 <= precision <= 18 (Biscotti uses
+ * PRECISION = 4, main.go:45). */
+int bk_quantized_sum_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
+                            int64_t ld, const int64_t *d_idx, int64_t m, int precision,
+                            int64_t *d_sum, double *d_sum_float);
+
+/* Noise application (client DP step) -- requestNoiseFromNoisers
+ * (DistSys/main.go:1606-1653: noiseVec = 0 + v_0 + ... + v_{k-1}, then
+ * /= float64(k)) and NoisedDelta = Delta + noise (main.go:1524-1537), batched
+ * over n updates:
+ *     out[i][c] = delta[i][c] + ((0 + noise[i][0][c]) + ... + noise[i][k-1][c]) / k
+ * noise vector j of update i starts at d_noise + (i*k + j) * noise_ld.  out may
+ * alias delta (out_ld == ld).  k = 0 gives NaN (0/0), as the Go code does. */
+int bk_noise_apply_device(bk_ctx *ctx, const double *d_delta, int64_t n, int64_t d, int64_t ld,
+                          const double *d_noise, int64_t k, int64_t noise_ld, double *d_out,
+                          int64_t out_ld);
+
 /* ---- measurement: per-kernel HIP-event timing on the context stream ------- */
 enum bk_kernel_id {
     BK_K_GRAM = 0,     /* K1  fp64-MFMA split-K upper-triangle Gram partials */
@@ -141,7 +182,10 @@ enum bk_kernel_id {
     BK_K_SYNTH = 8,
     BK_K_H2D = 9,
     BK_K_D2H = 10,
-    BK_NUM_KERNELS = 11
+    BK_K_AGGREGATE = 11, /* K4' block aggregation global += sum (bk_aggregate*) */
+    BK_K_QSUM = 12,      /* K5  quantised int64 sum (bk_quantized_sum_device)  */
+    BK_K_NOISE = 13,     /* K6  noise application (bk_noise_apply_device)      */
+    BK_NUM_KERNELS = 14
 };
 int bk_timing_enable(bk_ctx *ctx, int on);   /* clears accumulated timings */
 int bk_timing_read(bk_ctx *ctx, int kernel_id, double *total_ms, int64_t *count);

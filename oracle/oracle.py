@@ -49,6 +49,14 @@ def lib():
         L.oracle_synth_fill.restype = None
         L.oracle_synth_perm.argtypes = [ctypes.c_uint64, _i64, _vp]
         L.oracle_synth_perm.restype = None
+        L.oracle_aggregate.argtypes = [_vp, _i64, _i64, _vp, _i64, _vp]
+        L.oracle_aggregate.restype = None
+        L.oracle_qsum.argtypes = [_vp, _i64, _i64, _vp, _i64, ctypes.c_int, _vp, _vp]
+        L.oracle_qsum.restype = None
+        L.oracle_noise.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _i64]
+        L.oracle_noise.restype = None
+        L.oracle_go_f64_to_i64.argtypes = [ctypes.c_double]
+        L.oracle_go_f64_to_i64.restype = _i64
         L.oracle_num_threads.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [ctypes.c_int]
         L.oracle_set_threads.restype = None
@@ -153,3 +161,46 @@ def set_threads(t):
 
 def num_threads():
     return lib().oracle_num_threads()
+
+
+# ---- SURVEY.md §8(f) rows 2-3 (oracle/aggregate_oracle.c) -----------------
+def _f64(X):
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim != 2 or X.strides[1] != 8:
+        X = np.ascontiguousarray(X)
+    return X, X.strides[0] // 8
+
+
+def aggregate(X, idx, global_w):
+    """honest.go:360-375: returns global_w + X[idx[0]] + X[idx[1]] + ... (sequential)."""
+    X, ld = _f64(X)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    out = np.array(global_w, dtype=np.float64, copy=True)
+    lib().oracle_aggregate(_ptr(X), X.shape[1], ld, _ptr(idx), len(idx), _ptr(out))
+    return out
+
+
+def qsum(X, idx, precision=4):
+    """kyber.go:698-710 + 745-757: (int64 sum, float64 sum) of the quantised rows."""
+    X, ld = _f64(X)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    d = X.shape[1]
+    s = np.empty(d, dtype=np.int64)
+    sf = np.empty(d, dtype=np.float64)
+    lib().oracle_qsum(_ptr(X), d, ld, _ptr(idx), len(idx), int(precision), _ptr(s), _ptr(sf))
+    return s, sf
+
+
+def noise(delta, noise_vecs):
+    """main.go:1524-1537 + 1606-1653, batched: delta (n, d), noise (n, k, d)."""
+    D, ld = _f64(delta)
+    N = np.ascontiguousarray(noise_vecs, dtype=np.float64)
+    n, d = D.shape
+    k = N.shape[1]
+    out = np.empty((n, d), dtype=np.float64)
+    lib().oracle_noise(_ptr(D), n, d, ld, _ptr(N) if k else None, k, d, _ptr(out), d)
+    return out
+
+
+def go_f64_to_i64(y):
+    return lib().oracle_go_f64_to_i64(float(y))
