@@ -262,6 +262,12 @@ __device__ __forceinline__ void g3_wait(int vm) {
     }
 }
 
+// the same with the count known at compile time: one instruction, no branch tree
+template <int N>
+__device__ __forceinline__ void g3_waitc() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 __device__ __forceinline__ void g3_barrier() {
     // every wave's glds for the stage have landed (each waited for its own)
     __builtin_amdgcn_s_barrier();
@@ -349,7 +355,9 @@ __device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const d2v (&a)[4], con
 #else
 #define G3_PROBE(v) const long long v = 0
 #endif
-template <int KIND, int MODE, bool STAG>
+// NB > 0: the group stages exactly NB row-blocks (compile time: a single
+// s_waitcnt and straight-line glds); NB = 0: read G.nb at run time.
+template <int KIND, int MODE, bool STAG, int NB>
 __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld, int n, int nfull,
                                         int64_t d, const GroupDesc &G, const int *wd, char *lds,
                                         int wave, int lane, double *out, long long (&probe)[2]) {
@@ -357,7 +365,7 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
     int blk[G3_MAXB];
 #pragma unroll
     for (int b = 0; b < G3_MAXB; ++b) blk[b] = G.blk[b];
-    const int c = G.nb;  // glds per wave per k-block (8 per row-block, 8 waves)
+    const int c = NB > 0 ? NB : G.nb;  // glds per wave per k-block (8 per row-block, 8 waves)
     const int sA = G.task[wave][1], sB = G.task[wave][2];
     const int kst = wd[1], kstr = wd[2], kend = wd[3];
     const int nk = kst < kend ? (kend - 1 - kst) / kstr + 1 : 0;
@@ -384,8 +392,8 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
         const int64_t col = kb * G3_BK;
         char *base = lds + stage * G3_STAGE;
 #pragma unroll
-        for (int m = 0; m < G3_MAXB; ++m)
-            if (m < c)
+        for (int m = 0; m < (NB > 0 ? NB : G3_MAXB); ++m)
+            if (NB > 0 || m < c)
                 __builtin_amdgcn_global_load_lds((const void *)(gsrc[m] + col),
                                                  (void *)(base + gdst[m]), 16, 0, 0);
     };
@@ -414,7 +422,14 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
     for (int t = 0; t < nk; ++t) {
         const int ahead = min(nk - t - 1, G3_STAGES - 2);  // stages issued after t
         G3_PROBE(p0);
-        g3_wait(MODE == 2 ? 0 : ahead * c);
+        if constexpr (NB > 0 && MODE != 2) {
+            if (ahead > 0)
+                g3_waitc<NB>();
+            else
+                g3_waitc<0>();
+        } else {
+            g3_wait(MODE == 2 ? 0 : ahead * c);
+        }
         G3_PROBE(p1);
         g3_barrier();
         G3_PROBE(p2);
@@ -522,6 +537,29 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
 #ifndef G3_STAGGER
 #define G3_STAGGER 1
 #endif
+template <int MODE, int NB>
+__device__ __forceinline__ void g3_dispatch(const double *__restrict__ X, int64_t ld, int n,
+                                            int nfull, int64_t d, const GroupDesc &G,
+                                            const int *wd, char *lds, int wave, int lane,
+                                            double *out, long long (&probe)[2]) {
+    switch (G.task[wave][0]) {
+    case T_OFF:
+        if (wave >= 4 && G3_STAGGER)
+            g3_wave<T_OFF, MODE, true, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        else
+            g3_wave<T_OFF, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        break;
+    case T_PAIR:
+        g3_wave<T_PAIR, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        break;
+    case T_DIAG1:
+        g3_wave<T_DIAG1, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        break;
+    default:
+        g3_wave<T_NONE, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        break;
+    }
+}
 template <int MODE>
 __global__ __launch_bounds__(512, 2) void k_gram3(const double *__restrict__ X, int64_t ld, int n,
                                                   int nfull, int64_t d,
@@ -542,16 +580,17 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const double *__restrict__ X, 
     const GroupDesc &G = groups[wd[0]];
     double *out = part + ((int64_t)blockIdx.x * 16 + wave * 2) * 4096;
     long long probe[2] = {0, 0};
-    switch (G.task[wave][0]) {
-    case T_OFF:
-        if (wave >= 4 && G3_STAGGER)
-            g3_wave<T_OFF, MODE, true>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
-        else
-            g3_wave<T_OFF, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
-        break;
-    case T_PAIR: g3_wave<T_PAIR, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-    case T_DIAG1: g3_wave<T_DIAG1, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-    default: g3_wave<T_NONE, MODE, false>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+    if constexpr (MODE == 0) {
+        switch (G.nb) {
+        case 1: g3_dispatch<MODE, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 2: g3_dispatch<MODE, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 3: g3_dispatch<MODE, 3>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 4: g3_dispatch<MODE, 4>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 5: g3_dispatch<MODE, 5>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        default: g3_dispatch<MODE, 6>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        }
+    } else {
+        g3_dispatch<MODE, 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
     }
     if (trace) {
 #ifdef BK_K1_PROBE
