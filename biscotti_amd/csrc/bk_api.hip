@@ -91,6 +91,7 @@ struct bk_ctx {
     struct CachedPlan {
         int n;
         int64_t d;
+        int bk;  // columns per k-block (16 fp64, 32 fp32)
         Plan3 p;
     };
     std::vector<CachedPlan> plans;
@@ -205,13 +206,13 @@ void free_plan(Plan3 &p) {
     p.d_wg = p.d_red = p.d_wglist = nullptr;
 }
 
-int get_plan3(bk_ctx *c, int64_t n, int64_t d, Plan3 **out) {
+int get_plan3(bk_ctx *c, int64_t n, int64_t d, int bk, Plan3 **out) {
     for (auto &cp : c->plans)
-        if (cp.n == n && cp.d == d) {
+        if (cp.n == n && cp.d == d && cp.bk == bk) {
             *out = &cp.p;
             return BK_OK;
         }
-    Plan3Host H = build_plan3((int)n, d, c->num_cu);
+    Plan3Host H = build_plan3((int)n, d, c->num_cu, bk);
     for (int u = 0; u < H.ntile; ++u)
         if (H.red[3 * u + 1] < 0) return fail(BK_EHIP, "internal: K1 plan misses sub-tile %d", u);
     Plan3 p;
@@ -244,21 +245,25 @@ int get_plan3(bk_ctx *c, int64_t n, int64_t d, Plan3 **out) {
         free_plan(c->plans.front().p);
         c->plans.erase(c->plans.begin());
     }
-    c->plans.push_back({(int)n, d, p});
+    c->plans.push_back({(int)n, d, bk, p});
     *out = &c->plans.back().p;
     return BK_OK;
 }
 
+// K1 v3 reads 16-B granules with global_load_lds: every row start must be
+// 16-B aligned (fp64: ld even, fp32: ld a multiple of 4)
 bool use_v3(bk_ctx *c, const void *dX, int dtype, int64_t ld) {
-    return c->gram_variant == 3 && dtype == BK_F64 && (ld % 2) == 0 && ((uintptr_t)dX % 16) == 0;
+    const int64_t epg = dtype == BK_F64 ? 2 : 4;
+    return c->gram_variant == 3 && (ld % epg) == 0 && ((uintptr_t)dX % 16) == 0;
 }
+int v3_bk(int dtype) { return dtype == BK_F64 ? G3_BK : 2 * G3_BK; }
 
 // K1 + K1b: packed upper-triangle Gram of this call's columns into U
 int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
                double *U, Plan &pl) {
     if (use_v3(c, dX, dtype, ld)) {
         Plan3 *p3 = nullptr;
-        CHK(get_plan3(c, n, d, &p3));
+        CHK(get_plan3(c, n, d, v3_bk(dtype), &p3));
         pl.n = (int)n;
         pl.d = d;
         pl.T = p3->T;
@@ -274,8 +279,8 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
             trace = (long long *)c->trace.p;
         }
         CHK(timed(c, BK_K_GRAM, [&] {
-            return launch_gram3((const double *)dX, ld, (int)n, d, P3, part, c->stream,
-                                c->gram_mode, trace);
+            return launch_gram3(dX, dtype, ld, (int)n, d, P3, part, c->stream, c->gram_mode,
+                                trace);
         }));
         if (tfile) {
             std::vector<long long> h((size_t)P3.nwg * 24);

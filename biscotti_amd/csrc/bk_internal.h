@@ -58,9 +58,10 @@ struct Plan3Host {
     std::vector<int> red;     // 3 per sub-tile
     std::vector<int> wglist;  // concatenated per-group workgroup lists
 };
-Plan3Host build_plan3(int n, int64_t d, int num_cu);
+// bk = columns per k-block: 16 for fp64 input, 32 for fp32 (128 B per row either way)
+Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk = G3_BK);
 
-hipError_t launch_gram3(const double *X, int64_t ld, int n, int64_t d, const Plan3 &pl,
+hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl,
                         double *part, hipStream_t st, int mode = 0, long long *trace = nullptr);
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st);
 hipError_t configure_kernels();

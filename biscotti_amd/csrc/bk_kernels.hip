@@ -239,9 +239,32 @@ __global__ __launch_bounds__(256, 1) void k_gram(const T *__restrict__ X, int64_
 // lane-linearly) and on the read: conflict-free for ds_read_b128.
 // One s_barrier per 8-column k-block (64 MFMAs per SIMD in between).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ d2v g3_frag(const char *lds_blk, int q, int h, int rr, int g) {
+typedef float f4v __attribute__((ext_vector_type(4)));
+// One 16-byte LDS granule in the input type: 2 doubles or 4 floats.  A k-block
+// is 8 granules (128 B) per row: 16 fp64 columns or 32 fp32 columns, so the
+// LDS image, swizzle and glds shape are the same for both input types.
+template <typename T>
+struct G3T;
+template <>
+struct G3T<double> {
+    typedef d2v gran;
+    static constexpr int SUB = 2;   // MFMA sub-steps (k=4 each) per granule
+    static __device__ __forceinline__ double at(const d2v &v, int s) { return v[s]; }
+};
+template <>
+struct G3T<float> {
+    typedef f4v gran;
+    static constexpr int SUB = 4;
+    // fp32 -> fp64 is exact, and so is every fp32 x fp32 product in fp64
+    static __device__ __forceinline__ double at(const f4v &v, int s) { return (double)v[s]; }
+};
+
+template <typename T>
+__device__ __forceinline__ typename G3T<T>::gran g3_frag(const char *lds_blk, int q, int h, int rr,
+                                                         int g) {
     const int row = q * 16 + rr;
-    return *reinterpret_cast<const d2v *>(lds_blk + row * 128 + 16 * ((4 * h + g) ^ (row & 7)));
+    return *reinterpret_cast<const typename G3T<T>::gran *>(lds_blk + row * 128 +
+                                                            16 * ((4 * h + g) ^ (row & 7)));
 }
 
 __device__ __forceinline__ void g3_wait(int vm) {
@@ -302,15 +325,31 @@ __device__ __forceinline__ void diag_mma(d4v (&acc)[10], const d2v (&a)[4]) {
             for (int j = i; j < 4; ++j)
                 acc[dix(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][s], a[j][s], acc[dix(i, j)], 0, 0, 0);
 }
+// the same over one granule of either input type
+template <typename T>
+__device__ __forceinline__ void diag_mma_g(d4v (&acc)[10], const typename G3T<T>::gran (&a)[4]) {
+#pragma unroll
+    for (int s = 0; s < G3T<T>::SUB; ++s) {
+        double v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = G3T<T>::at(a[i], s);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i; j < 4; ++j)
+                acc[dix(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[i], v[j], acc[dix(i, j)], 0, 0, 0);
+    }
+}
 
-__device__ __forceinline__ void g3_load_rows(d2v (&a)[4], const double *__restrict__ X, int64_t ld,
+template <typename T>
+__device__ __forceinline__ void g3_load_rows(d2v (&a)[4], const T *__restrict__ X, int64_t ld,
                                              int n, int b, int64_t c, int64_t d, int rr) {
     // guarded direct loads for the ragged tail (c = first column of this lane)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const double *pr = X + (int64_t)min(b * 64 + q * 16 + rr, n - 1) * ld;
-        a[q].x = c < d ? pr[c] : 0.0;
-        a[q].y = c + 1 < d ? pr[c + 1] : 0.0;
+        const T *pr = X + (int64_t)min(b * 64 + q * 16 + rr, n - 1) * ld;
+        a[q].x = c < d ? (double)pr[c] : 0.0;
+        a[q].y = c + 1 < d ? (double)pr[c + 1] : 0.0;
     }
 }
 
@@ -333,14 +372,32 @@ __device__ __forceinline__ void store_diag(double *out, const d4v (&acc)[10], in
                 out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = j >= i ? acc[dix(i, j)][r] : 0.0;
 }
 
-// one MFMA sub-step s (columns 2g+s of the k-block) of an off-diagonal tile
-template <int S>
-__device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const d2v (&a)[4], const d2v (&b)[4]) {
+// one MFMA sub-step S (element S of each lane's granule) of an off-diagonal tile
+template <typename T, int S>
+__device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const typename G3T<T>::gran (&a)[4],
+                                        const typename G3T<T>::gran (&b)[4]) {
+    double va[4], vb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        va[i] = G3T<T>::at(a[i], S);
+        vb[i] = G3T<T>::at(b[i], S);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][S], b[j][S], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[i], vb[j], acc[i][j], 0, 0, 0);
+}
+// all SUB sub-steps of one granule
+template <typename T>
+__device__ __forceinline__ void off_mma_gran(d4v (&acc)[4][4], const typename G3T<T>::gran (&a)[4],
+                                             const typename G3T<T>::gran (&b)[4]) {
+    off_mma<T, 0>(acc, a, b);
+    off_mma<T, 1>(acc, a, b);
+    if constexpr (G3T<T>::SUB == 4) {
+        off_mma<T, 2>(acc, a, b);
+        off_mma<T, 3>(acc, a, b);
+    }
 }
 // STAG: waves 4-7 (the SIMD partners of waves 0-3) run their OFF tile half a
 // k-block behind -- the second 8-column half of block t-1 is issued after the
@@ -357,10 +414,13 @@ __device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const d2v (&a)[4], con
 #endif
 // NB > 0: the group stages exactly NB row-blocks (compile time: a single
 // s_waitcnt and straight-line glds); NB = 0: read G.nb at run time.
-template <int KIND, int MODE, bool STAG, int NB>
-__device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld, int n, int nfull,
+template <typename T, int KIND, int MODE, bool STAG, int NB>
+__device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int n, int nfull,
                                         int64_t d, const GroupDesc &G, const int *wd, char *lds,
                                         int wave, int lane, double *out, long long (&probe)[2]) {
+    typedef typename G3T<T>::gran gran;
+    constexpr int EPG = 16 / (int)sizeof(T);  // elements per 16-B granule
+    constexpr int BKE = 8 * EPG;               // columns per k-block (16 fp64, 32 fp32)
     const int rr = lane & 15, g = lane >> 4;
     int blk[G3_MAXB];
 #pragma unroll
@@ -374,7 +434,7 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
     // offsets; a stage only adds the k-block's column.  Instruction i of a stage
     // moves rows 8ii..8ii+7 (128 B each) of slot b = i/8; lane L takes row
     // 8ii + L/8, granule (L&7) of the LDS row <- global granule (L&7)^(row&7).
-    const double *gsrc[G3_MAXB];
+    const T *gsrc[G3_MAXB];
     int gdst[G3_MAXB];
     {
         const int rq = lane >> 3, j = lane & 7;
@@ -384,12 +444,12 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
             const int b = i >> 3, ii = i & 7;
             const int rl = ii * 8 + rq;
             const int grow = min(blk[b] * 64 + rl, n - 1);
-            gsrc[m] = X + (int64_t)grow * ld + 2 * (j ^ (rl & 7));
+            gsrc[m] = X + (int64_t)grow * ld + EPG * (j ^ (rl & 7));
             gdst[m] = b * G3_BLK + ii * 1024;
         }
     }
     auto issue = [&](int64_t kb, int stage) {
-        const int64_t col = kb * G3_BK;
+        const int64_t col = kb * BKE;
         char *base = lds + stage * G3_STAGE;
 #pragma unroll
         for (int m = 0; m < (NB > 0 ? NB : G3_MAXB); ++m)
@@ -411,9 +471,9 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
 #pragma unroll
         for (int i = 0; i < 10; ++i) acc.a[i] = d4v{0.0, 0.0, 0.0, 0.0};
     }
-    d2v ha[4], hb[4];  // STAG: the held second half of the previous k-block
+    gran ha[4], hb[4];  // STAG: the held second granule of the previous k-block
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ha[q] = hb[q] = d2v{0.0, 0.0};
+    for (int q = 0; q < 4; ++q) ha[q] = hb[q] = gran{};
 
 #pragma unroll
     for (int s = 0; s < G3_STAGES - 1; ++s)
@@ -445,24 +505,20 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
             continue;
         }
         if constexpr (KIND == T_OFF) {
-            d2v a0[4], b0[4], a1[4], b1[4];
+            gran a0[4], b0[4], a1[4], b1[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) a0[q] = g3_frag(ls + sA * G3_BLK, q, 0, rr, g);
+            for (int q = 0; q < 4; ++q) a0[q] = g3_frag<T>(ls + sA * G3_BLK, q, 0, rr, g);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) b0[q] = g3_frag(ls + sB * G3_BLK, q, 0, rr, g);
+            for (int q = 0; q < 4; ++q) b0[q] = g3_frag<T>(ls + sB * G3_BLK, q, 0, rr, g);
             if constexpr (STAG) {
-                if (t > 0) {
-                    off_mma<0>(acc.a, ha, hb);
-                    off_mma<1>(acc.a, ha, hb);
-                }
+                if (t > 0) off_mma_gran<T>(acc.a, ha, hb);
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) a1[q] = g3_frag(ls + sA * G3_BLK, q, 1, rr, g);
+            for (int q = 0; q < 4; ++q) a1[q] = g3_frag<T>(ls + sA * G3_BLK, q, 1, rr, g);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) b1[q] = g3_frag(ls + sB * G3_BLK, q, 1, rr, g);
+            for (int q = 0; q < 4; ++q) b1[q] = g3_frag<T>(ls + sB * G3_BLK, q, 1, rr, g);
             if (more) issue(nkb, nbuf);
-            off_mma<0>(acc.a, a0, b0);
-            off_mma<1>(acc.a, a0, b0);
+            off_mma_gran<T>(acc.a, a0, b0);
             if constexpr (STAG) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -470,49 +526,45 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
                     hb[q] = b1[q];
                 }
             } else {
-                off_mma<0>(acc.a, a1, b1);
-                off_mma<1>(acc.a, a1, b1);
+                off_mma_gran<T>(acc.a, a1, b1);
             }
         } else if constexpr (KIND == T_PAIR) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                d2v a[4], b[4];
+                gran a[4], b[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, h, rr, g);
+                for (int q = 0; q < 4; ++q) a[q] = g3_frag<T>(ls + sA * G3_BLK, q, h, rr, g);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) b[q] = g3_frag(ls + sB * G3_BLK, q, h, rr, g);
+                for (int q = 0; q < 4; ++q) b[q] = g3_frag<T>(ls + sB * G3_BLK, q, h, rr, g);
                 if (h == 0 && more) issue(nkb, nbuf);
-                diag_mma(acc.a, a);
-                diag_mma(acc.b, b);
+                diag_mma_g<T>(acc.a, a);
+                diag_mma_g<T>(acc.b, b);
             }
         } else if constexpr (KIND == T_DIAG1) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                d2v a[4];
+                gran a[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) a[q] = g3_frag(ls + sA * G3_BLK, q, h, rr, g);
+                for (int q = 0; q < 4; ++q) a[q] = g3_frag<T>(ls + sA * G3_BLK, q, h, rr, g);
                 if (h == 0 && more) issue(nkb, nbuf);
-                diag_mma(acc.a, a);
+                diag_mma_g<T>(acc.a, a);
             }
         } else {
             if (more) issue(nkb, nbuf);
         }
     }
     if constexpr (KIND == T_OFF && STAG && MODE != 1)
-        if (nk > 0) {
-            off_mma<0>(acc.a, ha, hb);
-            off_mma<1>(acc.a, ha, hb);
-        }
+        if (nk > 0) off_mma_gran<T>(acc.a, ha, hb);
     if constexpr (KIND != T_NONE) {
-        // ragged tail columns [nfull*16, d): one workgroup per group, direct loads
-        const int64_t c0 = (int64_t)nfull * G3_BK;
+        // ragged tail columns [nfull*BKE, d): one workgroup per group, direct loads
+        const int64_t c0 = (int64_t)nfull * BKE;
         if (wd[4] && c0 < d) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < BKE / 8; ++h) {
                 const int64_t cc = c0 + 8 * h + 2 * g;
                 d2v a[4], b[4];
-                g3_load_rows(a, X, ld, n, blk[sA], cc, d, rr);
-                g3_load_rows(b, X, ld, n, blk[sB], cc, d, rr);
+                g3_load_rows<T>(a, X, ld, n, blk[sA], cc, d, rr);
+                g3_load_rows<T>(b, X, ld, n, blk[sB], cc, d, rr);
                 if constexpr (KIND == T_OFF) {
                     gram_mma<false>(acc.a, a, b);
                 } else if constexpr (KIND == T_PAIR) {
@@ -537,31 +589,31 @@ __device__ __forceinline__ void g3_wave(const double *__restrict__ X, int64_t ld
 #ifndef G3_STAGGER
 #define G3_STAGGER 1
 #endif
-template <int MODE, int NB>
-__device__ __forceinline__ void g3_dispatch(const double *__restrict__ X, int64_t ld, int n,
+template <typename T, int MODE, int NB>
+__device__ __forceinline__ void g3_dispatch(const T *__restrict__ X, int64_t ld, int n,
                                             int nfull, int64_t d, const GroupDesc &G,
                                             const int *wd, char *lds, int wave, int lane,
                                             double *out, long long (&probe)[2]) {
     switch (G.task[wave][0]) {
     case T_OFF:
         if (wave >= 4 && G3_STAGGER)
-            g3_wave<T_OFF, MODE, true, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+            g3_wave<T, T_OFF, MODE, true, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         else
-            g3_wave<T_OFF, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+            g3_wave<T, T_OFF, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         break;
     case T_PAIR:
-        g3_wave<T_PAIR, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        g3_wave<T, T_PAIR, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         break;
     case T_DIAG1:
-        g3_wave<T_DIAG1, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        g3_wave<T, T_DIAG1, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         break;
     default:
-        g3_wave<T_NONE, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        g3_wave<T, T_NONE, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         break;
     }
 }
-template <int MODE>
-__global__ __launch_bounds__(512, 2) void k_gram3(const double *__restrict__ X, int64_t ld, int n,
+template <int MODE, typename T = double>
+__global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64_t ld, int n,
                                                   int nfull, int64_t d,
                                                   const GroupDesc *__restrict__ groups,
                                                   const int *__restrict__ wgtab,
@@ -582,15 +634,15 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const double *__restrict__ X, 
     long long probe[2] = {0, 0};
     if constexpr (MODE == 0) {
         switch (G.nb) {
-        case 1: g3_dispatch<MODE, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        case 2: g3_dispatch<MODE, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        case 3: g3_dispatch<MODE, 3>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        case 4: g3_dispatch<MODE, 4>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        case 5: g3_dispatch<MODE, 5>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        default: g3_dispatch<MODE, 6>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 1: g3_dispatch<T, MODE, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 2: g3_dispatch<T, MODE, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 3: g3_dispatch<T, MODE, 3>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 4: g3_dispatch<T, MODE, 4>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        case 5: g3_dispatch<T, MODE, 5>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+        default: g3_dispatch<T, MODE, 6>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
         }
     } else {
-        g3_dispatch<MODE, 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        g3_dispatch<T, MODE, 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
     }
     if (trace) {
 #ifdef BK_K1_PROBE
@@ -992,18 +1044,22 @@ hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, i
     return hipGetLastError();
 }
 
-hipError_t launch_gram3(const double *X, int64_t ld, int n, int64_t d, const Plan3 &pl,
+hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl,
                         double *part, hipStream_t st, int mode, long long *trace) {
     // mode != 0: timing-only ablations (1: no MFMA, 2: no global loads) -- wrong results
-    if (mode == 1)
-        hipLaunchKernelGGL(k_gram3<1>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
+    const dim3 grid((unsigned)pl.nwg), block(512);
+    if (dtype != 0)  // fp32 input: production mode only
+        hipLaunchKernelGGL((k_gram3<0, float>), grid, block, G3_LDS, st, (const float *)X, ld, n,
                            pl.nfull, d, pl.d_groups, pl.d_wg, part, trace);
+    else if (mode == 1)
+        hipLaunchKernelGGL(k_gram3<1>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
+                           d, pl.d_groups, pl.d_wg, part, trace);
     else if (mode == 2)
-        hipLaunchKernelGGL(k_gram3<2>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
-                           pl.nfull, d, pl.d_groups, pl.d_wg, part, trace);
+        hipLaunchKernelGGL(k_gram3<2>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
+                           d, pl.d_groups, pl.d_wg, part, trace);
     else
-        hipLaunchKernelGGL(k_gram3<0>, dim3((unsigned)pl.nwg), dim3(512), G3_LDS, st, X, ld, n,
-                           pl.nfull, d, pl.d_groups, pl.d_wg, part, trace);
+        hipLaunchKernelGGL(k_gram3<0>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
+                           d, pl.d_groups, pl.d_wg, part, trace);
     return hipGetLastError();
 }
 
@@ -1015,7 +1071,7 @@ hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStr
 
 hipError_t configure_kernels() {
     for (const void *k : {(const void *)k_gram3<0>, (const void *)k_gram3<1>,
-                          (const void *)k_gram3<2>}) {
+                          (const void *)k_gram3<2>, (const void *)k_gram3<0, float>}) {
         hipError_t e0 = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
         if (e0 != hipSuccess) return e0;
     }

@@ -93,13 +93,13 @@ GroupDesc make_group(int T, const std::vector<Task> &tasks) {
 
 }  // namespace
 
-Plan3Host build_plan3(int n, int64_t d, int num_cu) {
+Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
     Plan3Host H;
     const int T = (n + 63) / 64;
     const int TT = (T + 1) / 2;  // 128-row super-blocks
     H.T = T;
     H.ntile = T * (T + 1) / 2;
-    H.nfull = (int)(d / G3_BK);
+    H.nfull = (int)(d / bk);
 
     std::vector<std::vector<Task>> groups;  // each: 8 wave slots (waves w, w+4 pair on a SIMD)
     const Task none{T_NONE, 0, 0, 0};

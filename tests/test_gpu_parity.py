@@ -95,7 +95,10 @@ def test_gpu_generator_matches_cpu(engine, oracle):
     (2, 1, 1, 0, np.float64), (3, 7, 1, 1, np.float64), (64, 64, 20, 0, np.float64),
     (65, 129, 30, 2, np.float64), (128, 1000, 1, 0, np.float64), (200, 333, 198, 0, np.float64),
     (257, 2049, 77, 5, np.float32), (300, 40000, 90, 0, np.float32), (513, 4099, 153, 0, np.float64),
-    (40, 100003, 12, 0, np.float64)])
+    (40, 100003, 12, 0, np.float64),
+    # fp32 on K1 v3 (ld % 4 == 0): 32-column k-blocks, ragged tails, all-tail
+    (129, 4100, 40, 3, np.float32), (700, 32804, 210, 0, np.float32), (64, 28, 20, 0, np.float32),
+    (100, 7852, 30, 0, np.float32)])
 def test_against_oracle(engine, oracle, n, d, f, pad, dtype):
     X = oracle.synth(n, d, 1000 + n + d, max(0, min(f, n)), dtype=dtype)
     if pad:
