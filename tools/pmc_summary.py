@@ -5,7 +5,12 @@ global_load_dwordx4 and global_load_lds_dwordx4 alike -- so it is doubled for
 the kernels that read that way (k_gram3, k_mean); WRITE_SIZE is exact for
 16-B-per-lane stores and uncalibrated for narrower ones (noted, not scaled).
 
-    python tools/pmc_summary.py gpurun_out/prof_<tag> <workload> <out-prefix>
+    python tools/pmc_summary.py gpurun_out/prof_<tag> <workload> <out-prefix> [warmup steps]
+
+With warmup/steps (those of the profiled bench run, tools/profile.sh uses 1 and
+5) the K1 row also reports the mean over the timed window of dispatches from
+the per-dispatch kernel trace -- the figure bench.py's HIP events measure (the
+clock ramps over the first launches, so the all-call average runs high).
 """
 import collections
 import csv
@@ -13,7 +18,9 @@ import json
 import os
 import sys
 
-WIDE_READS = ("k_gram3", "k_mean", "k_gram<")
+# coalesced streaming readers (128-B requests tallied at 64 B): 16 B/lane, and
+# k_qsum's 8 B/lane (calibrated: doubled it equals m*d*8 exactly)
+WIDE_READS = ("k_gram3", "k_mean", "k_gram<", "k_noise", "k_qsum")
 
 
 def short(name):
@@ -75,6 +82,18 @@ def main():
     out_json = {"workload": workload, "source": prof, "kernels": res}
     if k1:
         out_json["k_gram"] = res[k1]
+        tr = os.path.join(prof, "trace", "run_kernel_trace.csv")
+        if len(sys.argv) > 5 and os.path.exists(tr):
+            w, st = int(sys.argv[4]), int(sys.argv[5])
+            durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                    for r in csv.DictReader(open(tr)) if short(r["Kernel_Name"]) == k1]
+            win = durs[w:w + st]
+            if win:
+                res[k1]["dispatch_ms"] = durs
+                res[k1]["timed_window_avg_ms"] = sum(win) / len(win)
+                lines += ["", "%s per dispatch (ms): %s" % (k1, " ".join("%.3f" % x for x in durs)),
+                          "timed window (dispatches %d..%d, = bench.py's timed steps): avg %.3f ms"
+                          % (w + 1, w + st, sum(win) / len(win))]
     json.dump(out_json, open(out + ".json", "w"), indent=1)
     open(out + ".md", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
