@@ -90,11 +90,12 @@ def cpu_baseline(w, target_s=10.0, target_1core_s=6.0):
 
 
 def next_rows(eng, X, n, d, sel, m, steps=5):
-    """SURVEY.md §8(f) rows 2-3 on the same device-resident batch (HBM-bound):
+    """SURVEY.md §8(f) rows 2-4 on the same device-resident batch (HBM-bound):
     block aggregation of the m selected rows into GlobalW (K4'), the
     secure-path quantised int64 sum (K5), and noise application to 128 of the
     updates with k = 2 noise vectors each (K6).  Algorithmic bytes:
-    aggregate m*d*8 + 2*d*8; qsum m*d*8 + 2*d*8; noise rows*d*8*(k+2)."""
+    aggregate m*d*8 + 2*d*8; qsum m*d*8 + 2*d*8; noise rows*d*8*(k+2).  Plus the
+    RONI verifier (row 4), batched over 512 updates."""
     import torch
     from biscotti_amd import _lib
     dev = X.device
@@ -122,6 +123,21 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
                     "NoisedDelta = Delta + mean of %d noise vectors, %d updates "
                     "(main.go:1524-1537, 1606-1653)" % (k, rows)),
     }
+    # RONI (§8(f) row 4): a creditcard-test-sized validation set (30% of
+    # 284,807 rows, d = 25: utils.py:86-117) scoring 512 updates in one launch
+    from biscotti_amd._lib import check, lib
+    nv, dr, nr = 85_000, 25, 512
+    g2 = torch.Generator(device=dev).manual_seed(5)
+    Xv = torch.randn((nv, dr), dtype=torch.float64, device=dev, generator=g2)
+    yv = torch.where(torch.randn(nv, dtype=torch.float64, device=dev, generator=g2) > 0, 1.0, -1.0)
+    ww = torch.randn(dr, dtype=torch.float64, device=dev, generator=g2)
+    dl = torch.randn((nr, dr), dtype=torch.float64, device=dev, generator=g2) * 1e-2
+    rs = torch.empty(nr, dtype=torch.float64, device=dev)
+    runs["k_roni"] = (lambda: check(lib().bk_roni_device(eng.ctx, Xv.data_ptr(), nv, dr, dr,
+                                                         yv.data_ptr(), ww.data_ptr(),
+                                                         dl.data_ptr(), nr, dr, rs.data_ptr())),
+                      None, "RONI scores of %d updates on a %d x %d validation set "
+                            "(logistic_validator.py:22-33)" % (nr, nv, dr))
     res = {}
     for name, (fn, nbytes, what) in runs.items():
         fn()
@@ -133,6 +149,11 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
         t = eng.timing_read().get(name)
         eng.timing_enable(False)
         ms = t["avg_ms"]
+        if nbytes is None:  # RONI: latency / L2-bound, reported as a rate
+            res[name] = {"what": what, "ms": round(ms, 4),
+                         "updates_per_s": round(nr / (ms * 1e-3), 1),
+                         "validation_dots_per_s": round(nv * (nr + 1) / (ms * 1e-3), 1)}
+            continue
         gbs = nbytes / (ms * 1e-3) / 1e9
         res[name] = {"what": what, "ms": round(ms, 4), "bytes": nbytes, "GB_per_s": round(gbs, 1),
                      "roofline": {"bound": "hbm", "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -16,7 +16,7 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 KERNELS = ["k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean",
-           "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise"]
+           "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni"]
 K = {name: i for i, name in enumerate(KERNELS)}
 
 # every symbol include/bk.h declares: name -> (restype, argtypes)
@@ -57,6 +57,9 @@ SIGNATURES = {
     "bk_aggregate": (_i, [_p, _p, _i, _i, _i64, _i64, _i64, _p, _i64, _p]),
     "bk_quantized_sum_device": (_i, [_p, _p, _i, _i64, _i64, _i64, _p, _i64, _i, _p, _p]),
     "bk_noise_apply_device": (_i, [_p, _p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64]),
+    "bk_roni_device": (_i, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _i64, _i64, _p]),
+    "bk_roni_set_validation": (_i, [_p, _p, _i64, _i64, _i64, _p]),
+    "bk_roni": (_i, [_p, _p, _p, _i64, _i64, _i64, _p]),
 }
 
 _lib = None

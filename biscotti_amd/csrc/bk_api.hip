@@ -58,7 +58,8 @@ int fail(int code, const char *fmt, ...) {
 const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_expand", "k_scores",
                                             "k_rank",    "k_compact", "k_mean",   "allreduce",
                                             "k_synth",   "h2d",       "d2h",
-                                            "k_aggregate", "k_qsum",  "k_noise"};
+                                            "k_aggregate", "k_qsum",  "k_noise",
+                                            "k_roni"};
 
 struct DevBuf {
     void *p = nullptr;
@@ -75,6 +76,9 @@ struct bk_ctx {
     std::mutex mu;
     // workspace (grow-only)
     DevBuf part, U, Ug, G, diag, scores, mask, sel, X, mean, perm, trace, idx;
+    // RONI: the validation set (bk_roni_set_validation) and per-call scratch
+    DevBuf roni_X, roni_y, roni_w, roni_d, roni_cnt, roni_s;
+    int64_t roni_nv = 0, roni_dim = 0;
     // host-side pinned allocations handed out by bk_stage_alloc
     std::vector<void *> staged;
     // timing
@@ -421,7 +425,8 @@ void bk_destroy(bk_ctx *c) {
         DeviceGuard dg(c->device);
         (void)hipStreamSynchronize(c->stream);
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->G,    &c->diag, &c->scores,
-                          &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx};
+                          &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
+                          &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s};
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
         for (void *p : c->staged) (void)hipHostFree(p);
@@ -840,4 +845,89 @@ int bk_noise_apply_device(bk_ctx *c, const double *d_delta, int64_t n, int64_t d
         return launch_noise(d_delta, ld, n, d, d_noise, k, noise_ld, d_out, out_ld, c->num_cu,
                             c->stream);
     });
+}
+
+// ---- RONI ------------------------------------------
+static int check_roni(int64_t nv, int64_t d, int64_t ldv, int64_t n, int64_t ld) {
+    if (nv < 1 || d < 1) return fail(BK_EINVAL, "need nv >= 1 and d >= 1");
+    if (ldv < d) return fail(BK_EINVAL, "ldv=%lld < d=%lld", (long long)ldv, (long long)d);
+    if (n < 0) return fail(BK_EINVAL, "n=%lld < 0", (long long)n);
+    if (n > 0 && ld < d) return fail(BK_EINVAL, "ld=%lld < d=%lld", (long long)ld, (long long)d);
+    if (d > 8192) return fail(BK_ENOTSUP, "RONI d=%lld exceeds 8192", (long long)d);
+    if (n > 65534) return fail(BK_ENOTSUP, "RONI n=%lld exceeds 65534", (long long)n);
+    return BK_OK;
+}
+
+int bk_roni_device(bk_ctx *c, const double *d_Xv, int64_t nv, int64_t d, int64_t ldv,
+                   const double *d_yv, const double *d_ww, const double *d_deltas, int64_t n,
+                   int64_t ld, double *d_scores) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    CHK(check_roni(nv, d, ldv, n, ld));
+    if (!d_Xv || !d_yv || !d_ww || (n > 0 && (!d_deltas || !d_scores)))
+        return fail(BK_EINVAL, "null pointer argument");
+    if (n == 0) return BK_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
+    unsigned int *cnt = (unsigned int *)c->roni_cnt.p;
+    return timed(c, BK_K_RONI, [&] {
+        return launch_roni(d_Xv, nv, d, ldv, d_yv, d_ww, d_deltas, n, ld, cnt, d_scores, c->stream);
+    });
+}
+
+int bk_roni_set_validation(bk_ctx *c, const double *Xv, int64_t nv, int64_t d, int64_t ldv,
+                           const double *yv) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    CHK(check_roni(nv, d, ldv, 0, d));
+    if (!Xv || !yv) return fail(BK_EINVAL, "null Xv / yv");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    CHK(ensure(c->roni_X, (size_t)nv * d * sizeof(double)));
+    CHK(ensure(c->roni_y, (size_t)nv * sizeof(double)));
+    HIPCHK(hipMemcpy2DAsync(c->roni_X.p, (size_t)d * sizeof(double), Xv, (size_t)ldv * sizeof(double),
+                            (size_t)d * sizeof(double), (size_t)nv, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->roni_y.p, yv, (size_t)nv * sizeof(double), hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->roni_nv = nv;
+    c->roni_dim = d;
+    return BK_OK;
+}
+
+int bk_roni(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_t d, int64_t ld,
+            double *scores) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    if (c->roni_nv < 1) return fail(BK_EINVAL, "no validation set: call bk_roni_set_validation");
+    if (d != c->roni_dim)
+        return fail(BK_EINVAL, "d=%lld != validation set's %lld", (long long)d, (long long)c->roni_dim);
+    CHK(check_roni(c->roni_nv, d, d, n, ld));
+    if (!ww || (n > 0 && (!deltas || !scores))) return fail(BK_EINVAL, "null pointer argument");
+    if (n == 0) return BK_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    CHK(ensure(c->roni_w, (size_t)d * sizeof(double)));
+    CHK(ensure(c->roni_d, (size_t)n * d * sizeof(double)));
+    CHK(ensure(c->roni_s, (size_t)n * sizeof(double)));
+    CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
+    double *dw = (double *)c->roni_w.p, *dd = (double *)c->roni_d.p, *ds = (double *)c->roni_s.p;
+    CHK(timed(c, BK_K_H2D, [&] {
+        hipError_t e = hipMemcpyAsync(dw, ww, (size_t)d * sizeof(double), hipMemcpyHostToDevice,
+                                      c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpy2DAsync(dd, (size_t)d * sizeof(double), deltas, (size_t)ld * sizeof(double),
+                                 (size_t)d * sizeof(double), (size_t)n, hipMemcpyHostToDevice,
+                                 c->stream);
+        return e;
+    }));
+    CHK(timed(c, BK_K_RONI, [&] {
+        return launch_roni((const double *)c->roni_X.p, c->roni_nv, d, d,
+                           (const double *)c->roni_y.p, dw, dd, n, d,
+                           (unsigned int *)c->roni_cnt.p, ds, c->stream);
+    }));
+    CHK(timed(c, BK_K_D2H, [&] {
+        return hipMemcpyAsync(scores, ds, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
+                              c->stream);
+    }));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BK_OK;
 }

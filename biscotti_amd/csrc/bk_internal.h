@@ -87,6 +87,10 @@ hipError_t launch_noise(const double *delta, int64_t ld, int64_t n, int64_t d, c
                         int64_t k, int64_t nld, double *out, int64_t old, int num_cu,
                         hipStream_t st);
 hipError_t configure_aggregate_kernels();
+// bk_roni.hip
+hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, const double *yv,
+                       const double *ww, const double *deltas, int64_t n, int64_t ld,
+                       unsigned int *cnt, double *scores, hipStream_t st);
 hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, int64_t c0,
                         const int64_t *perm, const SynthParams &P, hipStream_t st);
 

@@ -1,0 +1,83 @@
+"""Host-side mirror of Biscotti's RONI verifier, on libbk.
+
+  roni(ww, delta)                 ML/code/logistic_validator.py:22-33 (the
+                                  validation set is the module's, set once
+                                  with set_validation -- the module body loads
+                                  it at import, :6-7)
+  RONIValidator                   Honest.verifyUpdate, DistSys/honest.go:598-629
+    .verify_update(update)        Peer.VerifyUpdateRONI, DistSys/main.go:191-233:
+                                  accept iff PRIV_PROB > 0 or score <= 0.02
+    .scores(ww, deltas)           the batched form (one launch for n updates)
+
+Everything runs through libbk.so on the GPU (bk_roni_set_validation / bk_roni);
+there is no CPU path.
+"""
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import check, lib
+from .krum import Engine, Update, default_engine
+
+__all__ = ["RONI_THRESHOLD", "RONIValidator", "set_validation", "roni"]
+
+RONI_THRESHOLD = 0.02  # main.go:213
+
+
+class RONIValidator:
+    """One validation set resident on one GPU (bk_roni_set_validation)."""
+
+    def __init__(self, Xvalid, yvalid, engine: Optional[Engine] = None, priv_prob: float = 0.0):
+        self._engine = engine if engine is not None else default_engine(0)
+        X = np.ascontiguousarray(Xvalid, dtype=np.float64)
+        y = np.ascontiguousarray(yvalid, dtype=np.float64)
+        if X.ndim != 2 or y.shape != (X.shape[0],):
+            raise ValueError("Xvalid must be (nv, d) and yvalid (nv,)")
+        self.nv, self.d = X.shape
+        self.priv_prob = priv_prob  # PRIV_PROB > 0 accepts every update (main.go:205-211)
+        check(lib().bk_roni_set_validation(self._engine.ctx, X.ctypes.data, self.nv, self.d,
+                                           self.d, y.ctypes.data))
+
+    def scores(self, ww, deltas) -> np.ndarray:
+        ww = np.ascontiguousarray(ww, dtype=np.float64)
+        D = np.ascontiguousarray(np.atleast_2d(deltas), dtype=np.float64)
+        if ww.shape != (self.d,) or D.shape[1] != self.d:
+            raise ValueError("ww must be (d,) and deltas (n, d) with d = %d" % self.d)
+        out = np.empty(D.shape[0], dtype=np.float64)
+        check(lib().bk_roni(self._engine.ctx, ww.ctypes.data, D.ctypes.data, D.shape[0], self.d,
+                            self.d, out.ctypes.data))
+        return out
+
+    def roni(self, ww, delta) -> float:
+        return float(self.scores(ww, np.asarray(delta)[None])[0])
+
+    def verify_update(self, update: Update, latest_gradient) -> bool:
+        """True = accept (sign), False = reject (updateError)."""
+        score = self.roni(latest_gradient, update.NoisedDelta)
+        if self.priv_prob > 0:
+            return True
+        return not (score > RONI_THRESHOLD)
+
+    def verify_updates(self, updates: Sequence[Update], latest_gradient) -> np.ndarray:
+        """The batched form: one launch scores every update."""
+        sc = self.scores(latest_gradient, np.stack([u.NoisedDelta for u in updates]))
+        if self.priv_prob > 0:
+            return np.ones(len(updates), dtype=bool)
+        return ~(sc > RONI_THRESHOLD)
+
+
+_validator: Optional[RONIValidator] = None
+
+
+def set_validation(Xvalid, yvalid, engine: Optional[Engine] = None):
+    """The module-level validation set (logistic_validator.py:6-7)."""
+    global _validator
+    _validator = RONIValidator(Xvalid, yvalid, engine)
+    return _validator
+
+
+def roni(ww, delta) -> float:
+    """logistic_validator.py:22-33 against the set given to set_validation."""
+    if _validator is None:
+        raise RuntimeError("call set_validation(Xvalid, yvalid) first (the module loads it)")
+    return _validator.roni(ww, delta)

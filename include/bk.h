@@ -169,6 +169,25 @@ int bk_noise_apply_device(bk_ctx *ctx, const double *d_delta, int64_t n, int64_t
                           const double *d_noise, int64_t k, int64_t noise_ld, double *d_out,
                           int64_t out_ld);
 
+/* RONI verifier -- roni(ww, delta),
+ * ML/code/logistic_validator.py:22-33, batched over n updates:
+ *     score[i] = mean(sign(Xv . (ww + delta_i)) != yv) - mean(sign(Xv . ww) != yv)
+ * with numpy's sign (0 -> 0, NaN -> NaN, which never equals a label).  Xv is
+ * nv x d (row stride ldv), yv the nv labels as doubles (creditcard: -1 / +1,
+ * utils.py:96-97), ww d weights, deltas n x d (row stride ld).  The Go verifier
+ * rejects an update whose score exceeds 0.02 (main.go:213-226).  d <= 8192,
+ * n <= 65534. */
+int bk_roni_device(bk_ctx *ctx, const double *d_Xv, int64_t nv, int64_t d, int64_t ldv,
+                   const double *d_yv, const double *d_ww, const double *d_deltas, int64_t n,
+                   int64_t ld, double *d_scores);
+/* The Go verifier's shape: the validation set is uploaded once per context
+ * (pyInit imports it with the module, honest.go:204-258), then verifyUpdate
+ * (honest.go:598-629) scores host updates against the chain's latest model. */
+int bk_roni_set_validation(bk_ctx *ctx, const double *Xv, int64_t nv, int64_t d, int64_t ldv,
+                           const double *yv);
+int bk_roni(bk_ctx *ctx, const double *ww, const double *deltas, int64_t n, int64_t d, int64_t ld,
+            double *scores);
+
 /* ---- measurement: per-kernel HIP-event timing on the context stream ------- */
 enum bk_kernel_id {
     BK_K_GRAM = 0,     /* K1  fp64-MFMA split-K upper-triangle Gram partials */
@@ -185,7 +204,8 @@ enum bk_kernel_id {
     BK_K_AGGREGATE = 11, /* K4' block aggregation global += sum (bk_aggregate*) */
     BK_K_QSUM = 12,      /* K5  quantised int64 sum (bk_quantized_sum_device)  */
     BK_K_NOISE = 13,     /* K6  noise application (bk_noise_apply_device)      */
-    BK_NUM_KERNELS = 14
+    BK_K_RONI = 14,      /* K7  RONI counts + scores (bk_roni*)                 */
+    BK_NUM_KERNELS = 15
 };
 int bk_timing_enable(bk_ctx *ctx, int on);   /* clears accumulated timings */
 int bk_timing_read(bk_ctx *ctx, int kernel_id, double *total_ms, int64_t *count);

@@ -55,6 +55,8 @@ def lib():
         L.oracle_qsum.restype = None
         L.oracle_noise.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _i64]
         L.oracle_noise.restype = None
+        L.oracle_roni.argtypes = [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _vp]
+        L.oracle_roni.restype = ctypes.c_int
         L.oracle_go_f64_to_i64.argtypes = [ctypes.c_double]
         L.oracle_go_f64_to_i64.restype = _i64
         L.oracle_num_threads.restype = ctypes.c_int
@@ -204,3 +206,17 @@ def noise(delta, noise_vecs):
 
 def go_f64_to_i64(y):
     return lib().oracle_go_f64_to_i64(float(y))
+
+
+# ---- SURVEY.md §8(f) row 4 (oracle/roni_oracle.c) -------------------------
+def roni(Xv, yv, ww, deltas):
+    """logistic_validator.py:22-33 for each row of deltas: scores (n,)."""
+    Xv = np.ascontiguousarray(Xv, dtype=np.float64)
+    yv = np.ascontiguousarray(yv, dtype=np.float64)
+    ww = np.ascontiguousarray(ww, dtype=np.float64)
+    D = np.ascontiguousarray(np.atleast_2d(deltas), dtype=np.float64)
+    nv, d = Xv.shape
+    out = np.empty(D.shape[0], dtype=np.float64)
+    assert lib().oracle_roni(_ptr(Xv), nv, d, d, _ptr(yv), _ptr(ww), _ptr(D), D.shape[0], d,
+                             _ptr(out)) == 0
+    return out

@@ -44,7 +44,7 @@ def test_abi_version_and_names():
     assert L.bk_abi_version() == 2
     assert L.bk_kernel_name(0) == b"k_gram"
     assert L.bk_kernel_name(99) == b"?"
-    assert len(_lib.KERNELS) == 14
+    assert len(_lib.KERNELS) == 15
     for i, name in enumerate(_lib.KERNELS):
         assert L.bk_kernel_name(i) == name.encode()
 
