@@ -853,7 +853,7 @@ static int check_roni(int64_t nv, int64_t d, int64_t ldv, int64_t n, int64_t ld)
     if (ldv < d) return fail(BK_EINVAL, "ldv=%lld < d=%lld", (long long)ldv, (long long)d);
     if (n < 0) return fail(BK_EINVAL, "n=%lld < 0", (long long)n);
     if (n > 0 && ld < d) return fail(BK_EINVAL, "ld=%lld < d=%lld", (long long)ld, (long long)d);
-    if (d > 8192) return fail(BK_ENOTSUP, "RONI d=%lld exceeds 8192", (long long)d);
+    if (d > 1024) return fail(BK_ENOTSUP, "RONI d=%lld exceeds 1024", (long long)d);
     if (n > 65534) return fail(BK_ENOTSUP, "RONI n=%lld exceeds 65534", (long long)n);
     return BK_OK;
 }
