@@ -75,7 +75,7 @@ struct bk_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace (grow-only)
-    DevBuf part, U, Ug, G, diag, scores, mask, sel, X, mean, perm, trace, idx;
+    DevBuf part, U, Ug, scores, mask, sel, X, mean, perm, trace, idx;
     // RONI: the validation set (bk_roni_set_validation) and per-call scratch
     DevBuf roni_X, roni_y, roni_w, roni_d, roni_cnt, roni_s;
     int64_t roni_nv = 0, roni_dim = 0;
@@ -308,25 +308,20 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
     return BK_OK;
 }
 
-// K1c + K2 + K3 + K4 from a packed upper Gram
+// K2 + K3 + K4 from a packed upper Gram
 int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int dtype,
                  int64_t n, int64_t d, int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
                  double *d_mean) {
-    CHK(ensure(c->G, (size_t)n * n * sizeof(double)));
-    CHK(ensure(c->diag, (size_t)n * sizeof(double)));
     CHK(ensure(c->mask, (size_t)n * sizeof(int)));
     double *sc = d_scores;
     if (!sc) {
         CHK(ensure(c->scores, (size_t)n * sizeof(double)));
         sc = (double *)c->scores.p;
     }
-    double *G = (double *)c->G.p, *diag = (double *)c->diag.p;
     int *mask = (int *)c->mask.p;
     const int64_t m = n - f;
     const int64_t k = n - f - 2 > 0 ? n - f - 2 : 0;
-    CHK(timed(c, BK_K_EXPAND,
-              [&] { return launch_expand(U, (int)n, pl.T, pl.ntile, G, diag, c->stream); }));
-    CHK(timed(c, BK_K_SCORES, [&] { return launch_scores(G, diag, (int)n, k, sc, c->stream); }));
+    CHK(timed(c, BK_K_SCORES, [&] { return launch_scores(U, pl.T, (int)n, k, sc, c->stream); }));
     CHK(timed(c, BK_K_RANK, [&] { return launch_rank(sc, (int)n, (int)m, mask, c->stream); }));
     CHK(timed(c, BK_K_COMPACT, [&] { return launch_compact(mask, (int)n, d_sel, c->stream); }));
     if (d_mean && d > 0)
@@ -424,7 +419,7 @@ void bk_destroy(bk_ctx *c) {
         std::lock_guard<std::mutex> lk(c->mu);
         DeviceGuard dg(c->device);
         (void)hipStreamSynchronize(c->stream);
-        DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->G,    &c->diag, &c->scores,
+        DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->scores,
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s};
         for (DevBuf *b : bufs)

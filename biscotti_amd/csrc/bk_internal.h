@@ -69,9 +69,7 @@ hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, c
                        double *part, hipStream_t st);
 hipError_t launch_reduce(const double *part, const Plan &pl, double *U, hipStream_t st);
 hipError_t launch_sum_ranks(const double *Ug, int R, int64_t stride, double *U, hipStream_t st);
-hipError_t launch_expand(const double *U, int n, int T, int ntile, double *G, double *diag,
-                         hipStream_t st);
-hipError_t launch_scores(const double *G, const double *diag, int n, int64_t k, double *scores,
+hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores,
                          hipStream_t st);
 hipError_t launch_rank(const double *scores, int n, int m, int *mask, hipStream_t st);
 hipError_t launch_compact(const int *mask, int n, int64_t *sel, hipStream_t st);

@@ -5,8 +5,8 @@
 //                   v_mfma_f64_16x16x4_f64 (the -2XX^T term of
 //                   logistic_validator.py:59-60; norms come from its diagonal)
 //   K1b k_reduce    fixed-order sum of the split-K partials -> packed upper
-//   K1c k_expand    packed upper -> symmetric G (n x n) + diag
-//   K2  k_scores    per row: D_ij = (G_ii + G_jj) - 2 G_ij, bitonic sort in LDS
+//   K2  k_scores    per row: D_ij = (G_ii + G_jj) - 2 G_ij read straight from the
+//                   packed upper tiles (no n x n expansion), bitonic sort in LDS
 //                   (NaN last), sum of ranks 1..k      (logistic_validator.py:62-63)
 //   K3  k_rank      rank of each score (ties -> lower index, NaN last), mask
 //   K3b k_compact   mask -> ascending selected indices (argpartition set, :45)
@@ -730,44 +730,33 @@ __global__ __launch_bounds__(256) void k_sum_ranks(const double *__restrict__ Ug
 }
 
 // ---------------------------------------------------------------------------
-// K1c: packed upper -> symmetric G (n x n, row-major) + diag
-// grid: ntile*16 blocks; upper elements only (diagonal sub-tiles: i <= j)
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_expand(const double *__restrict__ U, int n, int T_,
-                                                double *__restrict__ G, double *__restrict__ diag) {
-    const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
-    int bi, bj;
-    tri_decode(u, T_, bi, bj);
-    const int i = chunk * 4 + (threadIdx.x >> 6), j = threadIdx.x & 63;
-    const int r = bi * 64 + i, c = bj * 64 + j;
-    if (r >= n || c >= n) return;
-    if (bi == bj && j < i) return;
-    const double v = U[(int64_t)u * 4096 + i * 64 + j];
-    G[(int64_t)r * n + c] = v;
-    if (r != c)
-        G[(int64_t)c * n + r] = v;
-    else
-        diag[r] = v;
-}
-
-// ---------------------------------------------------------------------------
 // K2: score[i] = sum of ranks 1..k of sort(D[i])   (logistic_validator.py:62-63)
 // One workgroup per row; the row lives in LDS as order-preserving u64 keys.
 // ---------------------------------------------------------------------------
+// G_ij straight from the packed upper 64x64 tiles (K1b's output): tiles below
+// the diagonal and the lower half of diagonal tiles read the transposed
+// element -- the same values the former K1c expansion copied, so bit-identical
+__device__ __forceinline__ int64_t upper_tile(int T, int a, int b) {
+    return (int64_t)(a * T - a * (a - 1) / 2 + (b - a)) * 4096;
+}
+__device__ __forceinline__ double u_at(const double *__restrict__ U, int T, int r, int c) {
+    const int br = r >> 6, bc = c >> 6, ir = r & 63, ic = c & 63;
+    if (br < bc || (br == bc && ir <= ic)) return U[upper_tile(T, br, bc) + ir * 64 + ic];
+    return U[upper_tile(T, bc, br) + ic * 64 + ir];
+}
+
 template <int NT>
-__global__ __launch_bounds__(NT) void k_scores(const double *__restrict__ G,
-                                               const double *__restrict__ diag, int n, int npow2,
-                                               int64_t k, double *__restrict__ scores) {
+__global__ __launch_bounds__(NT) void k_scores(const double *__restrict__ U, int T_, int n,
+                                               int npow2, int64_t k, double *__restrict__ scores) {
     extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
     __shared__ double red[NT / 64];
     const int i = blockIdx.x, tid = threadIdx.x;
-    const double di = diag[i];
-    const double *Gi = G + (int64_t)i * n;
+    const double di = u_at(U, T_, i, i);
     for (int j = tid; j < npow2; j += NT) {
         uint64_t key = ~0ULL;  // padding sorts after every real value (NaN included)
         if (j < n) {
-            const double t = di + diag[j];
-            const double g2 = 2.0 * Gi[j];
+            const double t = di + u_at(U, T_, j, j);
+            const double g2 = 2.0 * u_at(U, T_, i, j);
             key = dkey(t - g2);
         }
         keys[j] = key;
@@ -806,23 +795,23 @@ __global__ __launch_bounds__(NT) void k_scores(const double *__restrict__ G,
 // ---------------------------------------------------------------------------
 // K3: rank_i = #{j : key_j < key_i} + #{j < i : key_j == key_i}; mask = rank < m
 // ---------------------------------------------------------------------------
+// one wave per row: lanes sweep j, a ballot counts the keys ranked before i
 __global__ __launch_bounds__(256) void k_rank(const double *__restrict__ scores, int n, int m,
                                               int *__restrict__ mask) {
-    __shared__ uint64_t sk[2048];
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const uint64_t ki = (i < n) ? dkey(scores[i]) : 0ULL;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= n) return;  // wave-uniform
+    const uint64_t ki = dkey(scores[i]);
     int cnt = 0;
-    for (int base = 0; base < n; base += 2048) {
-        const int len = min(2048, n - base);
-        __syncthreads();
-        for (int j = threadIdx.x; j < len; j += 256) sk[j] = dkey(scores[base + j]);
-        __syncthreads();
-        for (int j = 0; j < len; ++j) {
-            const uint64_t kj = sk[j];
-            cnt += (kj < ki) || (kj == ki && base + j < i);
+    for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        bool before = false;
+        if (j < n) {
+            const uint64_t kj = dkey(scores[j]);
+            before = (kj < ki) || (kj == ki && j < i);
         }
+        cnt += __popcll(__ballot(before));
     }
-    if (i < n) mask[i] = cnt < m ? 1 : 0;
+    if (lane == 0) mask[i] = cnt < m ? 1 : 0;
 }
 
 // K3b: ascending compaction of mask (single workgroup of 1024 threads)
@@ -953,32 +942,26 @@ hipError_t launch_sum_ranks(const double *Ug, int R, int64_t stride, double *U, 
     return hipGetLastError();
 }
 
-hipError_t launch_expand(const double *U, int n, int T, int ntile, double *G, double *diag,
-                         hipStream_t st) {
-    hipLaunchKernelGGL(k_expand, dim3((unsigned)ntile * 16), dim3(256), 0, st, U, n, T, G, diag);
-    return hipGetLastError();
-}
-
 static int next_pow2(int v) {
     int p = 1;
     while (p < v) p <<= 1;
     return p;
 }
 
-hipError_t launch_scores(const double *G, const double *diag, int n, int64_t k, double *scores,
+hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores,
                          hipStream_t st) {
     const int np2 = next_pow2(n < 2 ? 2 : n);
     const size_t lds = (size_t)np2 * sizeof(uint64_t);
     if (np2 <= 2048) {
-        hipLaunchKernelGGL(k_scores<256>, dim3(n), dim3(256), lds, st, G, diag, n, np2, k, scores);
+        hipLaunchKernelGGL(k_scores<256>, dim3(n), dim3(256), lds, st, U, T, n, np2, k, scores);
     } else {
-        hipLaunchKernelGGL(k_scores<1024>, dim3(n), dim3(1024), lds, st, G, diag, n, np2, k, scores);
+        hipLaunchKernelGGL(k_scores<1024>, dim3(n), dim3(1024), lds, st, U, T, n, np2, k, scores);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_rank(const double *scores, int n, int m, int *mask, hipStream_t st) {
-    hipLaunchKernelGGL(k_rank, dim3((n + 255) / 256), dim3(256), 0, st, scores, n, m, mask);
+    hipLaunchKernelGGL(k_rank, dim3((n + 3) / 4), dim3(256), 0, st, scores, n, m, mask);
     return hipGetLastError();
 }
 

@@ -237,6 +237,16 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
             slots.push(t1);
             mk = std::max(mk, t1);
         }
+        // + the split-K reduce (K1b) reading every workgroup's partial slabs
+        // after K1, in cost units: bytes / ~4 TB/s / (256 cycles at ~2.25 GHz)
+        double slab_bytes = 0;
+        for (int g = 0; g < ng; ++g) {
+            double b = 0;
+            for (int w = 0; w < 8; ++w)
+                b += G[g].task[w][0] == T_PAIR ? 65536.0 : G[g].task[w][0] != T_NONE ? 32768.0 : 0.0;
+            slab_bytes += b * Q[g] * NX;
+        }
+        mk += slab_bytes / 4e12 / (256.0 / 2.25e9);
         if (mk < best * 0.995) {
             best = mk;
             bestQ = Q;

@@ -201,8 +201,9 @@ def test_timing_api(engine):
         _dev_run(engine, X, f)
     t = engine.timing_read()
     engine.timing_enable(False)
-    for k in ("k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean"):
+    for k in ("k_gram", "k_reduce", "k_scores", "k_rank", "k_compact", "k_mean"):
         assert t[k]["count"] == 3 and t[k]["avg_ms"] > 0
+    assert "k_expand" not in t  # fused into k_scores (reads the packed upper tiles)
 
 
 @pytest.mark.parametrize("deterministic", [False, True])
