@@ -50,6 +50,7 @@ SIGNATURES = {
     "bk_synth_fill_device": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _i64, _u64, _i64, _d, _d,
                                   _d, _i]),
     "bk_timing_enable": (_i, [_p, _i]),
+    "bk_timing_select": (_i, [_p, ctypes.c_uint32]),
     "bk_timing_read": (_i, [_p, _i, _pd, _pi64]),
     "bk_kernel_name": (ctypes.c_char_p, [_i]),
     "bk_plan": (_i, [_p, _i64, _i64, _pi64, _pi64, _pi64, _pi64]),

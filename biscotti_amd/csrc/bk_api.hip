@@ -82,7 +82,7 @@ struct bk_ctx {
     // host-side pinned allocations handed out by bk_stage_alloc
     std::vector<void *> staged;
     // timing
-    bool timing = false;
+    uint32_t timing = 0;  // bit k: record HIP events around kernel k (bk_timing_select)
     struct Ev {
         int kid;
         hipEvent_t a, b;
@@ -138,10 +138,13 @@ int get_event(bk_ctx *c, hipEvent_t *out) {
 }
 
 // Bracket one launch with events when timing is on.
+bool timing_on(const bk_ctx *c, int kid) { return (c->timing >> kid) & 1u; }
+
 template <typename F>
 int timed(bk_ctx *c, int kid, F &&launch) {
     hipEvent_t a = nullptr, b = nullptr;
-    if (c->timing) {
+    const bool on = timing_on(c, kid);
+    if (on) {
         CHK(get_event(c, &a));
         CHK(get_event(c, &b));
         HIPCHK(hipEventRecord(a, c->stream));
@@ -149,7 +152,7 @@ int timed(bk_ctx *c, int kid, F &&launch) {
     hipError_t e = launch();
     if (e != hipSuccess)
         return fail(BK_EHIP, "%s launch: %s", kKernelNames[kid], hipGetErrorString(e));
-    if (c->timing) {
+    if (on) {
         HIPCHK(hipEventRecord(b, c->stream));
         c->pending.push_back({kid, a, b});
     }
@@ -483,11 +486,13 @@ int bk_stage_free(bk_ctx *c, void *p) {
 int bk_plan(bk_ctx *c, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *ntile,
             int64_t *nwg) {
     if (n < 1 || d < 1) return fail(BK_EINVAL, "need n, d >= 1");
-    const Plan pl = make_plan(n, d, c ? c->num_cu : 256, (size_t)n * d * 8);
-    if (S) *S = pl.S;
-    if (kc) *kc = pl.kc;
-    if (ntile) *ntile = pl.ntile;
-    if (nwg) *nwg = pl.nwg;
+    if (n > BK_MAX_N) return fail(BK_ENOTSUP, "n=%lld exceeds BK_MAX_N=%d", (long long)n, BK_MAX_N);
+    // the K1 v3 plan for aligned fp64 rows (host tables only, nothing allocated)
+    const Plan3Host H = build_plan3((int)n, d, c ? c->num_cu : 256, G3_BK);
+    if (S) *S = (int64_t)H.groups.size();
+    if (kc) *kc = G3_BK;
+    if (ntile) *ntile = H.ntile;
+    if (nwg) *nwg = (int64_t)(H.wg.size() / 5);
     return BK_OK;
 }
 
@@ -624,13 +629,13 @@ int bk_multikrum_sharded_device(bk_ctx *c, const void *dX, int dtype, int64_t n,
     if (c->comm) {  // also at 1 rank, so the exchange is exercised on a 1-GPU box
         if (!c->deterministic) {
             hipEvent_t a = nullptr, b = nullptr;
-            if (c->timing) {
+            if (timing_on(c, BK_K_ALLREDUCE)) {
                 CHK(get_event(c, &a));
                 CHK(get_event(c, &b));
                 HIPCHK(hipEventRecord(a, c->stream));
             }
             RCCLCHK(ncclAllReduce(U, U, (size_t)usz, ncclDouble, ncclSum, c->comm, c->stream));
-            if (c->timing) {
+            if (timing_on(c, BK_K_ALLREDUCE)) {
                 HIPCHK(hipEventRecord(b, c->stream));
                 c->pending.push_back({BK_K_ALLREDUCE, a, b});
             }
@@ -638,14 +643,14 @@ int bk_multikrum_sharded_device(bk_ctx *c, const void *dX, int dtype, int64_t n,
             CHK(ensure(c->Ug, (size_t)usz * c->nranks * sizeof(double)));
             double *Ug = (double *)c->Ug.p;
             hipEvent_t a = nullptr, b = nullptr;
-            if (c->timing) {
+            if (timing_on(c, BK_K_ALLREDUCE)) {
                 CHK(get_event(c, &a));
                 CHK(get_event(c, &b));
                 HIPCHK(hipEventRecord(a, c->stream));
             }
             RCCLCHK(ncclAllGather(U, Ug, (size_t)usz, ncclDouble, c->comm, c->stream));
             HIPCHK(launch_sum_ranks(Ug, c->nranks, usz, U, c->stream));
-            if (c->timing) {
+            if (timing_on(c, BK_K_ALLREDUCE)) {
                 HIPCHK(hipEventRecord(b, c->stream));
                 c->pending.push_back({BK_K_ALLREDUCE, a, b});
             }
@@ -696,6 +701,10 @@ int bk_synth_fill_device(bk_ctx *c, void *dX, int dtype, int64_t n, int64_t dl, 
 }
 
 int bk_timing_enable(bk_ctx *c, int on) {
+    return bk_timing_select(c, on ? ~0u : 0u);
+}
+
+int bk_timing_select(bk_ctx *c, uint32_t mask) {
     if (!c) return fail(BK_EINVAL, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
@@ -709,7 +718,7 @@ int bk_timing_enable(bk_ctx *c, int on) {
         c->tot_ms[i] = 0;
         c->cnt[i] = 0;
     }
-    c->timing = on != 0;
+    c->timing = mask;
     return BK_OK;
 }
 

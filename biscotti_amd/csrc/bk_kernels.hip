@@ -670,28 +670,40 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64
 }
 
 // K1b v3: U[u] = sum over the owning group's workgroups (fixed order) of its slab
+// block = 32 elements of one sub-tile x 8 interleaved sub-lists of its
+// workgroups' slabs (sub-list q sums slabs q, q+8, q+16, ... in order), then
+// the 8 sub-sums in order: a fixed order (deterministic), with 8x the loads in
+// flight of one serial chain -- small-n plans have ~256 slabs per sub-tile
 __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part,
                                                  const int *__restrict__ red,
                                                  const int *__restrict__ wglist,
                                                  double *__restrict__ U) {
-    const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
-    const int e = chunk * 256 + threadIdx.x;
+    __shared__ double sub[8][32];
+    const int u = blockIdx.x >> 7, el = threadIdx.x & 31, q = threadIdx.x >> 5;
+    const int e = (blockIdx.x & 127) * 32 + el;
     const int off = red[3 * u], np = red[3 * u + 1], slot = red[3 * u + 2];
     const int *wl = wglist + off;
     double acc = 0.0;
-    int s = 0;
-    for (; s + 4 <= np; s += 4) {
+    int s = q;
+    for (; s + 24 < np; s += 32) {
         const double v0 = part[((int64_t)wl[s + 0] * 16 + slot) * 4096 + e];
-        const double v1 = part[((int64_t)wl[s + 1] * 16 + slot) * 4096 + e];
-        const double v2 = part[((int64_t)wl[s + 2] * 16 + slot) * 4096 + e];
-        const double v3 = part[((int64_t)wl[s + 3] * 16 + slot) * 4096 + e];
+        const double v1 = part[((int64_t)wl[s + 8] * 16 + slot) * 4096 + e];
+        const double v2 = part[((int64_t)wl[s + 16] * 16 + slot) * 4096 + e];
+        const double v3 = part[((int64_t)wl[s + 24] * 16 + slot) * 4096 + e];
         acc += v0;
         acc += v1;
         acc += v2;
         acc += v3;
     }
-    for (; s < np; ++s) acc += part[((int64_t)wl[s] * 16 + slot) * 4096 + e];
-    U[(int64_t)u * 4096 + e] = acc;
+    for (; s < np; s += 8) acc += part[((int64_t)wl[s] * 16 + slot) * 4096 + e];
+    sub[q][el] = acc;
+    __syncthreads();
+    if (q == 0) {
+        double t = sub[0][el];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) t += sub[k][el];
+        U[(int64_t)u * 4096 + e] = t;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1047,7 +1059,7 @@ hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, 
 }
 
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st) {
-    hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 16), dim3(256), 0, st, part, pl.d_red,
+    hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 128), dim3(256), 0, st, part, pl.d_red,
                        pl.d_wglist, U);
     return hipGetLastError();
 }

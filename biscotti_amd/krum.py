@@ -163,6 +163,13 @@ class Engine:
     def timing_enable(self, on=True):
         check(lib().bk_timing_enable(self._ctx, 1 if on else 0))
 
+    def timing_select(self, kernels):
+        """Time only these kernels (names from _lib.KERNELS)."""
+        mask = 0
+        for k in kernels:
+            mask |= 1 << _lib.K[k]
+        check(lib().bk_timing_select(self._ctx, mask))
+
     def timing_read(self):
         out = {}
         for i, name in enumerate(_lib.KERNELS):

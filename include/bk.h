@@ -207,11 +207,15 @@ enum bk_kernel_id {
     BK_K_RONI = 14,      /* K7  RONI counts + scores (bk_roni*)                 */
     BK_NUM_KERNELS = 15
 };
-int bk_timing_enable(bk_ctx *ctx, int on);   /* clears accumulated timings */
+int bk_timing_enable(bk_ctx *ctx, int on);   /* all kernels; clears accumulated timings */
+/* Time only the kernels whose bit (1u << kernel_id) is set: every timed kernel
+ * adds two event records to the stream.  Clears accumulated timings. */
+int bk_timing_select(bk_ctx *ctx, uint32_t kernel_mask);
 int bk_timing_read(bk_ctx *ctx, int kernel_id, double *total_ms, int64_t *count);
 const char *bk_kernel_name(int kernel_id);
-/* The split-K plan K1 uses for a shape: pieces S, piece length kc (columns),
- * 64x64 upper sub-tiles ntile, workgroups nwg. */
+/* The K1 plan for an aligned fp64 shape: S = workgroup groups (row-block
+ * sets, bk_plan.hip), kc = columns per k-block, ntile = 64x64 upper sub-tiles,
+ * nwg = workgroups of the launch.  Host-side only; ctx may be NULL. */
 int bk_plan(bk_ctx *ctx, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *ntile,
             int64_t *nwg);
 
