@@ -175,6 +175,33 @@ def test_sharded_decomposition_equals_full(engine):
     assert np.array_equal(sel2.cpu().numpy(), fsel)
 
 
+@pytest.mark.parametrize("n,d,f,nsh", [(300, 50000, 90, 4), (700, 65536, 210, 8)])
+def test_sharded_decomposition_fp32(engine, oracle, n, d, f, nsh):
+    """Config E's form (fp32 updates, d sharded over ranks): per-shard fp32 Grams
+    (K1 v3, 32-column k-blocks) summed == the oracle on the exact fp64 widening."""
+    from biscotti_amd.dist import all_shards
+    X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F32, n, d, d, 0, d, 11, f)
+    usz = int(_lib.lib().bk_upper_elems(n))
+    acc = torch.zeros(usz, dtype=torch.float64, device="cuda")
+    for c0, dl in all_shards(d, nsh):
+        U = torch.empty(usz, dtype=torch.float64, device="cuda")
+        Xs = X[:, c0:c0 + dl]
+        engine.gram_upper_ptr(Xs.data_ptr(), _lib.BK_F32, n, dl, X.stride(0), U.data_ptr())
+        engine.synchronize()
+        acc += U
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    mean = torch.empty(d, dtype=torch.float64, device="cuda")
+    engine.finish_ptr(acc.data_ptr(), X.data_ptr(), _lib.BK_F32, n, d, d, f, sel.data_ptr(),
+                      None, mean.data_ptr())
+    engine.synchronize()
+    Xh = X.cpu().numpy()
+    osel, _, omean = oracle.krum(Xh, f)
+    assert np.array_equal(sel.cpu().numpy(), osel)
+    mscale = np.max(np.mean(np.abs(Xh[osel].astype(np.float64)), axis=0))
+    assert np.max(np.abs(mean.cpu().numpy() - omean)) <= 1e-9 * mscale
+
+
 def test_validator_end_to_end(engine, oracle):
     from biscotti_amd.krum import KRUMValidator, Update, get_krum_scores, krum, krum_mean
     X = oracle.synth(10, 25, 20261016, 2)
