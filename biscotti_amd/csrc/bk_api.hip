@@ -489,6 +489,8 @@ int bk_plan(bk_ctx *c, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *n
     if (n > BK_MAX_N) return fail(BK_ENOTSUP, "n=%lld exceeds BK_MAX_N=%d", (long long)n, BK_MAX_N);
     // the K1 v3 plan for aligned fp64 rows (host tables only, nothing allocated)
     const Plan3Host H = build_plan3((int)n, d, c ? c->num_cu : 256, G3_BK);
+    for (int u = 0; u < H.ntile; ++u)
+        if (H.red[3 * u + 1] < 0) return fail(BK_EHIP, "internal: K1 plan fails its coverage check");
     if (S) *S = (int64_t)H.groups.size();
     if (kc) *kc = G3_BK;
     if (ntile) *ntile = H.ntile;

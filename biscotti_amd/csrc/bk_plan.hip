@@ -184,10 +184,15 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
 
     // (3) XCD-aware pieces.  Workgroups b and b+8 share an XCD (dispatch is
     //     round-robin; speed only, never correctness).  XCD x owns k-blocks
-    //     [K_x, K_x+1); each group g runs Q_g workgroups per XCD, workgroup q
-    //     taking k-blocks K_x + q, + Q_g, ... so all groups on an XCD sweep the
-    //     same columns together and re-read shared row-blocks from its L2.
-    //     Q_g ~ cost_g (per-SIMD MFMA units per k-block) balances the groups.
+    //     [K_x, K_x+1), cut into R consecutive sub-ranges, one per dispatch
+    //     round.  In round r group g runs Q_g workgroups, workgroup q taking
+    //     k-blocks K_xr + q, + Q_g, ... < K_x(r+1), so within a round every
+    //     group on an XCD sweeps the same sub-range with its column front
+    //     level with the others', and the row-blocks the groups share are
+    //     re-read from the XCD's L2 instead of HBM.  (Strided over the whole
+    //     XCD range instead, a k-block would be read by one group in round 1
+    //     and by another in round 2: v7 fetched 2x the unique bytes.)
+    //     BK_PLAN_ALIGN=0 restores that v7 interleave for A/B runs.
     const int nfull = H.nfull;
     constexpr int NX = 8;
     const int per_xcd = std::max(1, num_cu / NX);
@@ -199,14 +204,20 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
     const double wg_overhead = ev ? atof(ev) : 100.0;
     const char *er = getenv("BK_PLAN_ROUNDS");
     const int force_rounds = er ? atoi(er) : 0;
+    const char *ea = getenv("BK_PLAN_ALIGN");
+    const bool aligned = ea ? atoi(ea) != 0 : true;
     double best = 1e300;
+    int bestR = 1;
     std::vector<int> bestQ(ng, 1);
     for (int rounds = 1; rounds <= 16; rounds *= 2) {
         if (force_rounds && rounds != force_rounds) continue;
-        const double slots_total = (double)rounds * per_xcd;
-        if (ng > slots_total * 4) continue;
-        // min-max apportionment of the XCD's slots (Q_g >= 1): repeatedly give a
-        // slot to the group with the largest eff_g / Q_g.  Equal eff_g / Q_g both
+        // aligned: Q_g workgroups per round on the XCD's slots; v7: Q_g over
+        // all rounds' slots at once
+        const double slots_total = aligned ? (double)std::max(per_xcd, ng)
+                                           : (double)rounds * per_xcd;
+        if (!aligned && ng > slots_total * 4) continue;
+        // min-max apportionment of the slots (Q_g >= 1): repeatedly give a slot
+        // to the group with the largest eff_g / Q_g.  Equal eff_g / Q_g both
         // balances the workgroups and makes every group's column front advance
         // at the same speed (shared row-blocks stay in L2).
         std::vector<int> Q(ng, 1);
@@ -220,14 +231,18 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
                 pq.push({eff_cost(G[g]) / Q[g], g});
             }
         }
-        // list-schedule one XCD's workgroups (largest first) on per_xcd slots
+        // list-schedule one XCD's workgroups in dispatch order on per_xcd slots
         std::vector<double> jobs;
-        const int64_t R = K[1] - K[0];
-        for (int g = 0; g < ng; ++g)
-            for (int q = 0; q < Q[g]; ++q) {
-                const int64_t nk = q < R ? (R - 1 - q) / Q[g] + 1 : 0;
-                jobs.push_back((double)nk * eff_cost(G[g]) + wg_overhead);
-            }
+        const int nr = aligned ? rounds : 1;
+        for (int r = 0; r < nr; ++r) {
+            const int64_t R = aligned ? (K[1] - K[0]) * (r + 1) / rounds - (K[1] - K[0]) * r / rounds
+                                      : K[1] - K[0];
+            for (int g = 0; g < ng; ++g)
+                for (int q = 0; q < Q[g]; ++q) {
+                    const int64_t nk = q < R ? (R - 1 - q) / Q[g] + 1 : 0;
+                    jobs.push_back((double)nk * eff_cost(G[g]) + wg_overhead);
+                }
+        }
         std::priority_queue<double, std::vector<double>, std::greater<double>> slots;
         for (int i = 0; i < per_xcd; ++i) slots.push(0.0);
         double mk = 0;
@@ -244,24 +259,29 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
             double b = 0;
             for (int w = 0; w < 8; ++w)
                 b += G[g].task[w][0] == T_PAIR ? 65536.0 : G[g].task[w][0] != T_NONE ? 32768.0 : 0.0;
-            slab_bytes += b * Q[g] * NX;
+            slab_bytes += b * Q[g] * nr * NX;
         }
         mk += slab_bytes / 4e12 / (256.0 / 2.25e9);
         if (mk < best * 0.995) {
             best = mk;
             bestQ = Q;
+            bestR = nr;
         }
     }
-    // per-XCD launch lists, interleaved over groups; b = 8 j + x
+    // per-XCD launch lists (round-major, then q, then group); b = 8 j + x
     std::vector<std::vector<std::array<int, 5>>> lists(NX);
     int maxq = 0;
     for (int g = 0; g < ng; ++g) maxq = std::max(maxq, bestQ[g]);
     for (int x = 0; x < NX; ++x)
-        for (int q = 0; q < maxq; ++q)
-            for (int g = 0; g < ng; ++g)
-                if (q < bestQ[g])
-                    lists[x].push_back({g, (int)(K[x] + q), bestQ[g], (int)K[x + 1],
-                                        (x == 0 && q == 0) ? 1 : 0});
+        for (int r = 0; r < bestR; ++r) {
+            const int64_t span = K[x + 1] - K[x];
+            const int k0 = (int)(K[x] + span * r / bestR), k1 = (int)(K[x] + span * (r + 1) / bestR);
+            for (int q = 0; q < maxq; ++q)
+                for (int g = 0; g < ng; ++g)
+                    if (q < bestQ[g])
+                        lists[x].push_back({g, k0 + q, bestQ[g], k1,
+                                            (x == 0 && r == 0 && q == 0) ? 1 : 0});
+        }
     size_t maxlen = 0;
     for (auto &l : lists) maxlen = std::max(maxlen, l.size());
     std::vector<std::vector<int>> gw(ng);
@@ -279,9 +299,21 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
             }
         }
     for (int g = 0; g < ng; ++g) {
-        G[g].Q = bestQ[g];
+        G[g].Q = bestQ[g] * bestR;
         G[g].wg0 = (int)H.wglist.size();
         H.wglist.insert(H.wglist.end(), gw[g].begin(), gw[g].end());
+    }
+    // every (group, k-block) exactly once, and exactly one tail workgroup per group
+    bool covered = true;
+    {
+        std::vector<int> seen((size_t)ng * nfull, 0), tails(ng, 0);
+        for (size_t b = 0; b < H.wg.size() / 5; ++b) {
+            const int *e = &H.wg[5 * b];
+            for (int64_t k = e[1]; k < e[3]; k += e[2]) seen[(size_t)e[0] * nfull + k]++;
+            tails[e[0]] += e[4];
+        }
+        for (int v : seen) covered = covered && v == 1;
+        for (int v : tails) covered = covered && v == 1;
     }
     // (4) reduce table: sub-tile u -> its group's workgroups, slot wave * 2 + t
     H.red.assign((size_t)H.ntile * 3, 0);
@@ -298,6 +330,7 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
             }
     bool ok = true;
     for (auto &g : G) ok = ok && g.nb <= G3_MAXB;
+    ok = ok && covered;
     for (int u = 0; u < H.ntile; ++u)
         if (seen[u] != 1 || !ok) H.red[3 * u + 1] = -1;  // planner bug marker (checked by the caller)
     H.groups = G;

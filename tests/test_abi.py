@@ -81,6 +81,20 @@ def test_plan_fills_the_chip():
     assert v[0].value == 4  # two band quads + two off-diagonal pairs of super-tiles
 
 
+@pytest.mark.parametrize("align", ["1", "0"])
+def test_plan_covers_every_kblock_once(align, monkeypatch):
+    """The planner's own check (bk_plan.hip): every (group, k-block) pair is
+    owned by exactly one workgroup and every group has one ragged-tail
+    workgroup -- for the round-aligned column sub-ranges (default) and the v7
+    interleave (BK_PLAN_ALIGN=0), over shapes from tiny to BK_MAX_N."""
+    monkeypatch.setenv("BK_PLAN_ALIGN", align)
+    L = _lib.lib()
+    v = [ctypes.c_int64() for _ in range(4)]
+    for n, d in [(1, 1), (2, 16), (65, 100), (100, 7850), (300, 1000003), (512, 1 << 20),
+                 (512, 131072), (1000, 12345), (4096, 32768), (16384, 4096)]:
+        assert L.bk_plan(None, n, d, *[ctypes.byref(x) for x in v]) == 0, (n, d, _lib.last_error())
+
+
 def test_null_and_bad_arguments_do_not_crash():
     L = _lib.lib()
     assert L.bk_create(None, 0) == _lib.BK_EINVAL

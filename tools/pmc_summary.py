@@ -7,8 +7,8 @@ the kernels that read that way (k_gram3, k_mean); WRITE_SIZE is exact for
 
     python tools/pmc_summary.py gpurun_out/prof_<tag> <workload> <out-prefix> [warmup steps]
 
-With warmup/steps (those of the profiled bench run, tools/profile.sh uses 1 and
-5) the K1 row also reports the mean over the timed window of dispatches from
+With warmup/steps (those of the profiled trace run: bench.py defaults, 10 and
+40) the K1 row also reports the mean over the timed window of dispatches from
 the per-dispatch kernel trace -- the figure bench.py's HIP events measure (the
 clock ramps over the first launches, so the all-call average runs high).
 """
@@ -95,6 +95,14 @@ def main():
                           "timed window (dispatches %d..%d, = bench.py's timed steps): avg %.3f ms"
                           % (w + 1, w + st, sum(win) / len(win))]
     json.dump(out_json, open(out + ".json", "w"), indent=1)
+    if k1 and "hbm_bytes_per_launch" in res[k1]:
+        # the file bench.py reads its roofline "traffic" from
+        pj = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                          "pmc_%s.json" % workload)
+        json.dump({"workload": workload, "source": "%s.json (tools/profile.sh %s)"
+                   % (os.path.relpath(out, os.path.dirname(pj) + "/.."), os.path.basename(prof)),
+                   "k_gram": {k: v for k, v in res[k1].items() if k != "dispatch_ms"}},
+                  open(pj, "w"), indent=1)
     open(out + ".md", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
