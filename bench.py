@@ -197,6 +197,9 @@ def main():
                     help="multi-GPU: all-gather + fixed-order sum instead of all-reduce")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded path + RCCL communicator even at 1 rank")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="tuning aid on a 1-GPU box: run rank 0's column shard of an N-rank "
+                         "job (sharded path, 1-rank RCCL exchange); value is that rank's rate")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -222,7 +225,10 @@ def main():
     w = WORKLOADS[a.workload]
     n, d, f = w["n"], w["d"], w["f"]
     m = n - f
-    c0, dl = shard_bounds(d, world, rank)
+    emu = a.emulate_ranks if world == 1 and a.emulate_ranks > 1 else 0
+    if emu:
+        sharded = a.sharded = True
+    c0, dl = shard_bounds(d, emu or world, rank)
     tdt = torch.float32 if w["dtype"] == "f32" else torch.float64
     bdt = _lib.BK_F32 if w["dtype"] == "f32" else _lib.BK_F64
     es = 4 if w["dtype"] == "f32" else 8
@@ -284,7 +290,7 @@ def main():
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / a.steps * 1e3
-    value = n * d * es / (elapsed / a.steps) / 1e9
+    value = n * (dl if emu else d) * es / (elapsed / a.steps) / 1e9
 
     parity = golden_check(a.workload, sel.cpu().numpy(), mean[:dl].cpu().numpy(), c0, dl)
 
@@ -348,7 +354,8 @@ def main():
         "data": "synthetic (repo SplitMix64 spec, generated on device; DESIGN.md)",
         "config": {"workload": a.workload, "n": n, "d": d, "f": f, "m": m,
                    "parallelism": ("d-shard x%d + RCCL %s" % (world, "all-gather" if a.deterministic else "all-reduce"))
-                   if sharded else "1 GPU",
+                   if sharded and not emu else
+                   ("emulated rank 0 of %d (1 GPU)" % emu if emu else "1 GPU"),
                    "d_local": dl},
         "roofline": roof,
         "kernels_ms_avg": {k: round(v["avg_ms"], 5) for k, v in kbreak.items()},
@@ -357,10 +364,10 @@ def main():
     if variants:
         out["variants"] = variants
 
-    if rank == 0 and world == 1 and not a.no_next_rows and w["dtype"] == "f64":
+    if rank == 0 and world == 1 and not emu and not a.no_next_rows and w["dtype"] == "f64":
         out["next_rows"] = next_rows(eng, X, n, d, sel, m)
 
-    if rank == 0 and world == 1 and not a.no_e2e:
+    if rank == 0 and world == 1 and not emu and not a.no_e2e:
         # PCIe-inclusive rate: pinned host batch -> H2D -> Multi-Krum -> D2H of sel and mean
         import ctypes
         Xh = torch.empty((n, dl), dtype=tdt, pin_memory=True)
@@ -383,7 +390,7 @@ def main():
                                          selh, sel.cpu().numpy()))}
         del Xh
 
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not emu and not a.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(w)
         except Exception as e:  # the oracle is optional for the GPU number itself

@@ -33,9 +33,21 @@ __host__ __device__ __forceinline__ int64_t go_f64_to_i64(double y) {
     return INT64_MIN;
 }
 
+// used-once streaming reads: non-temporal (see ld2s in bk_kernels.hip)
 template <typename T>
 __device__ __forceinline__ double ldv(const T *p) {
+#ifndef BK_NO_NT
+    return (double)__builtin_nontemporal_load(p);
+#else
     return (double)*p;
+#endif
+}
+__device__ __forceinline__ d2v ldnt(const double *p) {
+#ifndef BK_NO_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
+#else
+    return *reinterpret_cast<const d2v *>(p);
+#endif
 }
 
 template <typename T, bool FLT>
@@ -82,7 +94,7 @@ __global__ __launch_bounds__(256) void k_noise(const double *delta, int64_t ld, 
                     d2v v[8];
 #pragma unroll
                     for (int q = 0; q < 8; ++q)
-                        v[q] = *reinterpret_cast<const d2v *>(nz + (j + q) * nld + c);
+                        v[q] = ldnt(nz + (j + q) * nld + c);
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
                         s.x += v[q].x;
@@ -90,11 +102,11 @@ __global__ __launch_bounds__(256) void k_noise(const double *delta, int64_t ld, 
                     }
                 }
                 for (; j < k; ++j) {
-                    const d2v v = *reinterpret_cast<const d2v *>(nz + j * nld + c);
+                    const d2v v = ldnt(nz + j * nld + c);
                     s.x += v.x;
                     s.y += v.y;
                 }
-                const d2v a = *reinterpret_cast<const d2v *>(delta + i * ld + c);
+                const d2v a = ldnt(delta + i * ld + c);
                 d2v o;
                 o.x = a.x + s.x / dk;
                 o.y = a.y + s.y / dk;

@@ -82,6 +82,22 @@ __device__ __forceinline__ d2v ld2(const T *p) {
     return r;
 }
 
+// Streaming read of data used once (K4 and its aggregation variant): a
+// non-temporal load.  K4 at config D: 0.549 -> 0.495 ms (5.5 -> 6.1 TB/s,
+// profiles/r01/ab_mean_nt.log).  -DBK_NO_NT restores plain loads for A/B.
+template <typename T, bool VEC>
+__device__ __forceinline__ d2v ld2s(const T *p) {
+#ifndef BK_NO_NT
+    if constexpr (VEC && std::is_same<T, double>::value) {
+        return __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
+    } else if constexpr (VEC) {
+        const f2v v = __builtin_nontemporal_load(reinterpret_cast<const f2v *>(p));
+        return d2v{(double)v.x, (double)v.y};
+    }
+#endif
+    return ld2<T, VEC>(p);
+}
+
 // ---------------------------------------------------------------------------
 // K1: split-K upper-triangle Gram on fp64 MFMA.
 //
@@ -443,7 +459,11 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
             const int i = wave + 8 * m;
             const int b = i >> 3, ii = i & 7;
             const int rl = ii * 8 + rq;
+#ifdef BK_K1_SAMEROWS  // timing-only ablation: every slot reads row-block 0 (all L2 hits)
+            const int grow = min(rl, n - 1);
+#else
             const int grow = min(blk[b] * 64 + rl, n - 1);
+#endif
             gsrc[m] = X + (int64_t)grow * ld + EPG * (j ^ (rl & 7));
             gdst[m] = b * G3_BLK + ii * 1024;
         }
@@ -873,7 +893,7 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
             for (; r + 8 <= m; r += 8) {
                 d2v v[8];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) v[q] = ld2<T, VEC>(X + srow[r + q] + c);
+                for (int q = 0; q < 8; ++q) v[q] = ld2s<T, VEC>(X + srow[r + q] + c);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     acc.x += v[q].x;
@@ -881,7 +901,7 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
                 }
             }
             for (; r < m; ++r) {
-                const d2v v = ld2<T, VEC>(X + srow[r] + c);
+                const d2v v = ld2s<T, VEC>(X + srow[r] + c);
                 acc.x += v.x;
                 acc.y += v.y;
             }

@@ -257,3 +257,41 @@ def test_rccl_exchange_single_rank(engine, deterministic):
     assert np.array_equal(sc.cpu().numpy(), fsc)
     assert np.array_equal(mean.cpu().numpy(), fmean)
     e2.close()
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512,
+                               513, 777, 1023, 1024, 1025, 2049])
+def test_exact_ties_bitwise(engine, oracle, n):
+    """Integer-valued updates in {-1, 0, 1}: every Gram entry, distance and
+    score is an exact integer, so the GPU must agree with the oracle BITWISE
+    on the scores -- whatever the summation order -- and, with the heavy ties
+    this makes in distances and in scores, on the selected set under the
+    (value, index) total order (ties at the boundary go to the lower index)."""
+    rng = np.random.default_rng(1000 + n)
+    d = 40
+    X = rng.integers(-1, 2, size=(n, d)).astype(np.float64)
+    X[n // 2:n // 2 + max(1, n // 8)] = X[0]  # duplicated rows: zero distances, equal scores
+    for f in sorted({1, max(1, n // 3), max(1, n - 3), n - 1}):
+        if not 1 <= f < n:
+            continue
+        sel, sc, _ = engine.multikrum(X, f)
+        osel, osc, _ = oracle.krum(X, f)
+        assert np.array_equal(sel, osel), (n, f)
+        assert np.array_equal(sc, osc), (n, f)
+
+
+def test_nan_and_inf_rows(engine, oracle):
+    """NaN / Inf rows: NaN-aware score agreement with the oracle and the same
+    selection (NaN sorts last, as in numpy)."""
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((200, 64))
+    X[7] = np.nan
+    X[50, 3] = np.inf
+    X[120] = -np.inf
+    for f in (20, 60, 150):
+        sel, sc, _ = engine.multikrum(X, f)
+        osel, osc, _ = oracle.krum(X, f)
+        assert np.array_equal(sel, osel)
+        np.testing.assert_array_equal(np.isnan(sc), np.isnan(osc))
+        fin = np.isfinite(osc)
+        np.testing.assert_allclose(sc[fin], osc[fin], rtol=1e-12, atol=0)

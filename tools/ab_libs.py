@@ -8,7 +8,8 @@ interleaved on the same device buffer:
         nosum=biscotti_amd/libbk.so,BK_CSUM=0
 
 A ",KEY=VAL" suffix sets that env var while the build's context is created
-(the context reads BK_* knobs at bk_create).  Env: N, D, REPS.
+(the context reads BK_* knobs at bk_create).  Env: N, D, REPS, and F: with F
+set, time the whole bk_multikrum_device step and report K1 and K4 (k_mean).
 """
 import ctypes
 import os
@@ -73,6 +74,59 @@ def kgram_ms(lib, ctx, X, n, d, ld, U, reps=3):
     return ms.value / max(cnt.value, 1)
 
 
+def step_ms(lib, ctx, X, n, d, ld, f, sel, mean, reps=3):
+    lib.bk_multikrum_device(ctx, X, _lib.BK_F64, n, d, ld, f, sel, None, mean)
+    lib.bk_synchronize(ctx)
+    lib.bk_timing_enable(ctx, 1)
+    for _ in range(reps):
+        st = lib.bk_multikrum_device(ctx, X, _lib.BK_F64, n, d, ld, f, sel, None, mean)
+        assert st == 0, lib.bk_last_error()
+    lib.bk_synchronize(ctx)
+    out = []
+    for kid in (0, 6, 3, 1):
+        ms, cnt = ctypes.c_double(), ctypes.c_int64()
+        lib.bk_timing_read(ctx, kid, ctypes.byref(ms), ctypes.byref(cnt))
+        out.append(ms.value / max(cnt.value, 1))
+    lib.bk_timing_enable(ctx, 0)
+    # whole-step wall time with no events in the stream
+    import time
+    lib.bk_synchronize(ctx)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        lib.bk_multikrum_device(ctx, X, _lib.BK_F64, n, d, ld, f, sel, None, mean)
+    lib.bk_synchronize(ctx)
+    out.append((time.perf_counter() - t0) / 10 * 1e3)
+    return out
+
+
+def main_step(builds, X, n, d, f, reps):
+    m = n - f
+    res = {b[0]: [] for b in builds}
+    outs = {}
+    for label, lib, ctx, env in builds:
+        outs[label] = (torch.empty(m, dtype=torch.int64, device="cuda"),
+                       torch.empty(d, dtype=torch.float64, device="cuda"))
+    for _ in range(reps):
+        for label, lib, ctx, env in builds:
+            with _env(env):
+                sel, mean = outs[label]
+                res[label].append(step_ms(lib, ctx, X.data_ptr(), n, d, d, f, sel.data_ptr(),
+                                          mean.data_ptr()))
+    torch.cuda.synchronize()
+    ref = outs[builds[0][0]]
+    for label, v in res.items():
+        k1 = sorted(x[0] for x in v)[len(v) // 2]
+        k4 = sorted(x[1] for x in v)[len(v) // 2]
+        same = bool(torch.equal(outs[label][0], ref[0]) and torch.equal(outs[label][1], ref[1]))
+        k2 = sorted(x[2] for x in v)[len(v) // 2]
+        k1b = sorted(x[3] for x in v)[len(v) // 2]
+        stp = sorted(x[4] for x in v)[len(v) // 2]
+        print("%-8s n=%d d=%d f=%d step %.4f ms | K1 %.3f ms  K1b %.4f ms  K2 %.4f ms  K4 %.4f ms "
+              "(%.0f GB/s)  sel+mean==%s: %s" % (label, n, d, f, stp, k1, k1b, k2, k4,
+                                                 m * d * 8 / (k4 * 1e-3) / 1e9, builds[0][0], same),
+              flush=True)
+
+
 def main():
     n, d = int(os.environ.get("N", 512)), int(os.environ.get("D", 1 << 20))
     reps = int(os.environ.get("REPS", 8))
@@ -85,6 +139,8 @@ def main():
     lib0.bk_synth_fill_device(ctx0, X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 1, n // 3,
                               0.01, 0.05, 1e-3, 0)
     lib0.bk_synchronize(ctx0)
+    if os.environ.get("F"):
+        return main_step(builds, X, n, d, int(os.environ["F"]), reps)
     ue = int(lib0.bk_upper_elems(n))
     Us = {}
     for label, lib, ctx, env in builds:
