@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -462,7 +463,7 @@ int bk_stage_alloc(bk_ctx *c, int64_t bytes, void **pinned) {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     void *p = nullptr;
-    hipError_t e = hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, (size_t)bytes, hipHostMallocPortable);
     if (e != hipSuccess) return fail(BK_ENOMEM, "hipHostMalloc(%lld): %s", (long long)bytes,
                                      hipGetErrorString(e));
     c->staged.push_back(p);
@@ -659,6 +660,264 @@ int bk_multikrum_sharded_device(bk_ctx *c, const void *dX, int dtype, int64_t n,
         }
     }
     return stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, d_mean);
+}
+
+// ---- one process, G GPUs --------------------------------------------------
+}  // extern "C"
+
+struct bk_group {
+    std::vector<bk_ctx *> ctx;
+    int mode = BK_GROUP_ALLREDUCE;
+    std::mutex mu;
+    // per-rank device buffers of the call (shard of X, packed Gram, outputs)
+    std::vector<DevBuf> X, U, Ug, sel, sc, mean;
+    // BK_GROUP_HOST_EXCHANGE: pinned partials [G][usz] and their sum
+    void *hpart = nullptr, *hsum = nullptr;
+    size_t hbytes = 0;
+};
+
+namespace {
+
+// the column shard of rank r out of G (biscotti_amd/dist.py:shard_bounds)
+void group_shard(int64_t d, int G, int r, int64_t *c0, int64_t *dl) {
+    int64_t per = (d + G - 1) / G;
+    per = (per + 7) / 8 * 8;
+    const int64_t a = std::min<int64_t>(d, (int64_t)r * per);
+    const int64_t b = std::min<int64_t>(d, a + per);
+    *c0 = a;
+    *dl = b - a;
+}
+
+int group_free_host(bk_group *g) {
+    if (g->hpart) (void)hipHostFree(g->hpart);
+    if (g->hsum) (void)hipHostFree(g->hsum);
+    g->hpart = g->hsum = nullptr;
+    g->hbytes = 0;
+    return BK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bk_group_create(bk_group **out, int ngpus, const int *devices, int mode) {
+    if (!out) return fail(BK_EINVAL, "null out");
+    *out = nullptr;
+    if (ngpus < 1 || ngpus > 64) return fail(BK_EINVAL, "ngpus=%d out of range", ngpus);
+    if (mode < BK_GROUP_ALLREDUCE || mode > BK_GROUP_HOST_EXCHANGE)
+        return fail(BK_EINVAL, "bad group mode %d", mode);
+    std::vector<int> devs((size_t)ngpus);
+    for (int r = 0; r < ngpus; ++r) devs[(size_t)r] = devices ? devices[r] : r;
+    if (mode != BK_GROUP_HOST_EXCHANGE)
+        for (int a = 0; a < ngpus; ++a)
+            for (int b = a + 1; b < ngpus; ++b)
+                if (devs[(size_t)a] == devs[(size_t)b])
+                    return fail(BK_EINVAL, "RCCL group modes need distinct devices (device %d "
+                                           "repeats); use BK_GROUP_HOST_EXCHANGE",
+                                devs[(size_t)a]);
+    bk_group *g = new (std::nothrow) bk_group();
+    if (!g) return fail(BK_ENOMEM, "host allocation of bk_group failed");
+    g->mode = mode;
+    for (int r = 0; r < ngpus; ++r) {
+        bk_ctx *c = nullptr;
+        const int st = bk_create(&c, devs[(size_t)r]);
+        if (st != BK_OK) {
+            bk_group_destroy(g);
+            return st;
+        }
+        g->ctx.push_back(c);
+    }
+    const size_t G = (size_t)ngpus;
+    g->X.resize(G);
+    g->U.resize(G);
+    g->Ug.resize(G);
+    g->sel.resize(G);
+    g->sc.resize(G);
+    g->mean.resize(G);
+    if (mode != BK_GROUP_HOST_EXCHANGE) {
+        std::vector<ncclComm_t> comms(G, nullptr);
+        const ncclResult_t r = ncclCommInitAll(comms.data(), ngpus, devs.data());
+        if (r != ncclSuccess) {
+            bk_group_destroy(g);
+            return fail(BK_ERCCL, "ncclCommInitAll(%d): %s", ngpus, ncclGetErrorString(r));
+        }
+        for (int k = 0; k < ngpus; ++k) {  // each context owns (and destroys) its rank
+            g->ctx[(size_t)k]->comm = comms[(size_t)k];
+            g->ctx[(size_t)k]->nranks = ngpus;
+            g->ctx[(size_t)k]->rank = k;
+        }
+    }
+    *out = g;
+    return BK_OK;
+}
+
+void bk_group_destroy(bk_group *g) {
+    if (!g) return;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        bk_ctx *c = g->ctx[r];
+        {
+            DeviceGuard dg(c->device);
+            (void)hipStreamSynchronize(c->stream);
+            for (auto *v : {&g->X, &g->U, &g->Ug, &g->sel, &g->sc, &g->mean})
+                if (r < v->size() && (*v)[r].p) (void)hipFree((*v)[r].p);
+        }
+        bk_destroy(c);
+    }
+    group_free_host(g);
+    delete g;
+}
+
+int bk_group_size(const bk_group *g) { return g ? (int)g->ctx.size() : 0; }
+
+bk_ctx *bk_group_ctx(bk_group *g, int r) {
+    if (!g || r < 0 || r >= (int)g->ctx.size()) return nullptr;
+    return g->ctx[(size_t)r];
+}
+
+int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t n, int64_t d,
+                       int64_t ld, int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
+                       double *mean_out) {
+    if (!g || g->ctx.empty()) return fail(BK_EINVAL, "null group");
+    CHK(check_common(g->ctx[0], X, dtype, n, d, ld));
+    CHK(bk_check_args(n, d, f));
+    if (!sel_idx) return fail(BK_EINVAL, "null sel_idx");
+    if (where != BK_HOST && where != BK_HOST_PINNED)
+        return fail(BK_EINVAL, "bk_group_multikrum takes host X (where=%d)", where);
+    const int G = (int)g->ctx.size();
+    for (int r = 0; r < G; ++r) {
+        int64_t c0, dl;
+        group_shard(d, G, r, &c0, &dl);
+        if (dl < 1)  // d too small to give every device a column: one device does it all
+            return bk_multikrum(g->ctx[0], X, where, dtype, n, d, ld, f, sel_idx, m_out, scores,
+                                mean_out);
+    }
+    std::lock_guard<std::mutex> lk(g->mu);
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (bk_ctx *c : g->ctx) locks.emplace_back(c->mu);  // fixed order: no deadlock
+    const size_t es = esize(dtype);
+    const int64_t m = n - f;
+    const int64_t usz = bk_upper_elems(n);
+    std::vector<Plan> pls((size_t)G);
+    // 1. per device: H2D of its column shard, partial Gram (K1 + K1b)
+    for (int r = 0; r < G; ++r) {
+        bk_ctx *c = g->ctx[(size_t)r];
+        DeviceGuard dg(c->device);
+        int64_t c0, dl;
+        group_shard(d, G, r, &c0, &dl);
+        CHK(ensure(g->X[(size_t)r], (size_t)n * dl * es));
+        CHK(ensure(g->U[(size_t)r], (size_t)usz * sizeof(double)));
+        void *dst = g->X[(size_t)r].p;
+        const char *src = (const char *)X + (size_t)c0 * es;
+        CHK(timed(c, BK_K_H2D, [&] {
+            return hipMemcpy2DAsync(dst, (size_t)dl * es, src, (size_t)ld * es, (size_t)dl * es,
+                                    (size_t)n, hipMemcpyHostToDevice, c->stream);
+        }));
+        CHK(stage_gram(c, dst, dtype, n, dl, dl, (double *)g->U[(size_t)r].p, pls[(size_t)r]));
+    }
+    // 2. the exchange
+    if (g->mode == BK_GROUP_ALLREDUCE) {
+        RCCLCHK(ncclGroupStart());
+        for (int r = 0; r < G; ++r) {
+            bk_ctx *c = g->ctx[(size_t)r];
+            double *U = (double *)g->U[(size_t)r].p;
+            const ncclResult_t e =
+                ncclAllReduce(U, U, (size_t)usz, ncclDouble, ncclSum, c->comm, c->stream);
+            if (e != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return fail(BK_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(e));
+            }
+        }
+        RCCLCHK(ncclGroupEnd());
+    } else if (g->mode == BK_GROUP_DETERMINISTIC) {
+        for (int r = 0; r < G; ++r) {
+            DeviceGuard dg(g->ctx[(size_t)r]->device);
+            CHK(ensure(g->Ug[(size_t)r], (size_t)usz * G * sizeof(double)));
+        }
+        RCCLCHK(ncclGroupStart());
+        for (int r = 0; r < G; ++r) {
+            bk_ctx *c = g->ctx[(size_t)r];
+            const ncclResult_t e = ncclAllGather(g->U[(size_t)r].p, g->Ug[(size_t)r].p,
+                                                 (size_t)usz, ncclDouble, c->comm, c->stream);
+            if (e != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return fail(BK_ERCCL, "ncclAllGather: %s", ncclGetErrorString(e));
+            }
+        }
+        RCCLCHK(ncclGroupEnd());
+        for (int r = 0; r < G; ++r) {
+            bk_ctx *c = g->ctx[(size_t)r];
+            DeviceGuard dg(c->device);
+            HIPCHK(launch_sum_ranks((const double *)g->Ug[(size_t)r].p, G, usz,
+                                    (double *)g->U[(size_t)r].p, c->stream));
+        }
+    } else {  // host exchange: D2H partials, fixed rank-order sum, H2D
+        const size_t bytes = (size_t)usz * sizeof(double);
+        if (g->hbytes < bytes) {
+            group_free_host(g);
+            HIPCHK(hipHostMalloc(&g->hpart, bytes * G, hipHostMallocPortable));
+            HIPCHK(hipHostMalloc(&g->hsum, bytes, hipHostMallocPortable));
+            g->hbytes = bytes;
+        }
+        double *hp = (double *)g->hpart, *hs = (double *)g->hsum;
+        for (int r = 0; r < G; ++r) {
+            bk_ctx *c = g->ctx[(size_t)r];
+            DeviceGuard dg(c->device);
+            HIPCHK(hipMemcpyAsync(hp + (size_t)r * usz, g->U[(size_t)r].p, bytes,
+                                  hipMemcpyDeviceToHost, c->stream));
+        }
+        for (int r = 0; r < G; ++r) {
+            DeviceGuard dg(g->ctx[(size_t)r]->device);
+            HIPCHK(hipStreamSynchronize(g->ctx[(size_t)r]->stream));
+        }
+        for (int64_t e = 0; e < usz; ++e) {  // the order of k_sum_ranks: 0 + U_0 + U_1 + ...
+            double acc = 0.0;
+            for (int r = 0; r < G; ++r) acc += hp[(size_t)r * usz + e];
+            hs[e] = acc;
+        }
+        for (int r = 0; r < G; ++r) {
+            bk_ctx *c = g->ctx[(size_t)r];
+            DeviceGuard dg(c->device);
+            HIPCHK(hipMemcpyAsync(g->U[(size_t)r].p, hs, bytes, hipMemcpyHostToDevice, c->stream));
+        }
+    }
+    // 3. per device: scores + selection (identical everywhere), mean of its columns
+    for (int r = 0; r < G; ++r) {
+        bk_ctx *c = g->ctx[(size_t)r];
+        DeviceGuard dg(c->device);
+        int64_t c0, dl;
+        group_shard(d, G, r, &c0, &dl);
+        CHK(ensure(g->sel[(size_t)r], (size_t)n * sizeof(int64_t)));
+        CHK(ensure(g->sc[(size_t)r], (size_t)n * sizeof(double)));
+        double *dmean = nullptr;
+        if (mean_out) {
+            CHK(ensure(g->mean[(size_t)r], (size_t)dl * sizeof(double)));
+            dmean = (double *)g->mean[(size_t)r].p;
+        }
+        int64_t *dsel = (int64_t *)g->sel[(size_t)r].p;
+        double *dsc = (double *)g->sc[(size_t)r].p;
+        CHK(stage_finish(c, (const double *)g->U[(size_t)r].p, pls[(size_t)r], g->X[(size_t)r].p,
+                         dtype, n, dl, dl, f, dsel, dsc, dmean));
+        CHK(timed(c, BK_K_D2H, [&] {
+            hipError_t e = hipSuccess;
+            if (r == 0) {
+                e = hipMemcpyAsync(sel_idx, dsel, (size_t)m * sizeof(int64_t),
+                                   hipMemcpyDeviceToHost, c->stream);
+                if (e == hipSuccess && scores)
+                    e = hipMemcpyAsync(scores, dsc, (size_t)n * sizeof(double),
+                                       hipMemcpyDeviceToHost, c->stream);
+            }
+            if (e == hipSuccess && mean_out)
+                e = hipMemcpyAsync(mean_out + c0, dmean, (size_t)dl * sizeof(double),
+                                   hipMemcpyDeviceToHost, c->stream);
+            return e;
+        }));
+    }
+    for (int r = 0; r < G; ++r) {
+        DeviceGuard dg(g->ctx[(size_t)r]->device);
+        HIPCHK(hipStreamSynchronize(g->ctx[(size_t)r]->stream));
+    }
+    if (m_out) *m_out = m;
+    return BK_OK;
 }
 
 int bk_synth_fill_device(bk_ctx *c, void *dX, int dtype, int64_t n, int64_t dl, int64_t ld,

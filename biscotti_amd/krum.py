@@ -38,6 +38,71 @@ def _p(x):
     return ctypes.c_void_p(x) if x is not None else None
 
 
+def _as_rows(X):
+    X = np.asarray(X)
+    if X.dtype not in (np.float64, np.float32):
+        X = X.astype(np.float64)
+    if X.ndim != 2:
+        raise ValueError("deltas must be 2-D (n updates x d)")
+    if X.strides[1] != X.itemsize or X.strides[0] % X.itemsize:
+        X = np.ascontiguousarray(X)
+    return X
+
+
+class GroupEngine:
+    """One process driving G GPUs (bk_group_*): the Go verifier's multi-GPU
+    form.  Each device copies its column shard of the host batch over its own
+    PCIe link; the partial Grams are summed (RCCL all-reduce, RCCL all-gather
+    + fixed-order sum, or a fixed-order sum through pinned host memory); every
+    device selects identically and writes the mean of its columns."""
+
+    def __init__(self, devices, mode=_lib.BK_GROUP_ALLREDUCE):
+        devices = [int(x) for x in devices]
+        arr = (ctypes.c_int * len(devices))(*devices)
+        self._g = ctypes.c_void_p()
+        check(lib().bk_group_create(ctypes.byref(self._g), len(devices), arr, int(mode)))
+        self.devices = devices
+
+    def close(self):
+        if self._g:
+            lib().bk_group_destroy(self._g)
+            self._g = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def size(self):
+        return lib().bk_group_size(self._g)
+
+    def ctx(self, r):
+        return lib().bk_group_ctx(self._g, int(r))
+
+    def multikrum(self, X, f, want_scores=True, want_mean=True, pinned=False):
+        """bk_group_multikrum on a host batch: (sel ascending, scores, mean)."""
+        X = _as_rows(X)
+        n, d = X.shape
+        f = int(f)
+        check(lib().bk_check_args(n, d, f))
+        m = n - f
+        sel = np.empty(m, dtype=np.int64)
+        mo = ctypes.c_int64(0)
+        sc = np.empty(n, dtype=np.float64) if want_scores else None
+        mean = np.empty(d, dtype=np.float64) if want_mean else None
+        dt = _lib.BK_F32 if X.dtype == np.float32 else _lib.BK_F64
+        check(lib().bk_group_multikrum(self._g, X.ctypes.data,
+                                       _lib.BK_HOST_PINNED if pinned else _lib.BK_HOST, dt, n, d,
+                                       X.strides[0] // X.itemsize, f, sel.ctypes.data,
+                                       ctypes.addressof(mo),
+                                       sc.ctypes.data if sc is not None else None,
+                                       mean.ctypes.data if mean is not None else None))
+        assert mo.value == m
+        return sel, sc, mean
+
+
 class Engine:
     """One libbk context (bk_ctx) bound to one GPU."""
 

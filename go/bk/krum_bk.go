@@ -28,18 +28,34 @@ package main
 import "C"
 
 import (
+	"os"
+	"strconv"
 	"unsafe"
 )
 
 var (
-	bkCtx      *C.bk_ctx
+	bkCtx      *C.bk_ctx   // device 0's context (the group's rank 0 when bkGroup is set)
+	bkGroup    *C.bk_group // BK_GPUS > 1: one process driving that many GPUs
 	bkStage    unsafe.Pointer // C-owned pinned staging (cgo may not keep Go pointers)
 	bkStageLen int64
 )
 
-// initialize binds the engine instead of pyKRUMFunc (krum.go:31-44).
+// initialize binds the engine instead of pyKRUMFunc (krum.go:31-44).  With
+// BK_GPUS=G (G > 1) the verifier drives G GPUs from this one process: each
+// copies its column shard of the batch over its own PCIe link (bk_group_*).
 func (krumval *KRUMValidator) initialize() {
 	if bkCtx != nil {
+		return
+	}
+	if g, err := strconv.Atoi(os.Getenv("BK_GPUS")); err == nil && g > 1 {
+		var grp *C.bk_group
+		if st := C.bk_group_create(&grp, C.int(g), nil, C.BK_GROUP_ALLREDUCE); st != C.BK_OK {
+			outLog.Printf("bk_group_create(%d) failed (%d): %s", g, int(st),
+				C.GoString(C.bk_last_error()))
+			return
+		}
+		bkGroup, bkCtx = grp, C.bk_group_ctx(grp, 0)
+		outLog.Printf("Krum engine: libbk ABI %d on %d GPUs", int(C.bk_abi_version()), g)
 		return
 	}
 	var ctx *C.bk_ctx
@@ -93,8 +109,15 @@ func (krumval *KRUMValidator) getTopKRUMIndex(deltas [][]float64) []int {
 	m := n - f
 	sel := make([]C.int64_t, m)
 	var mOut C.int64_t
-	st := C.bk_multikrum(bkCtx, bkStage, C.BK_HOST_PINNED, C.BK_F64, C.int64_t(n), C.int64_t(d),
-		C.int64_t(d), C.int64_t(f), (*C.int64_t)(unsafe.Pointer(&sel[0])), &mOut, nil, nil)
+	var st C.int
+	if bkGroup != nil {
+		st = C.bk_group_multikrum(bkGroup, bkStage, C.BK_HOST_PINNED, C.BK_F64, C.int64_t(n),
+			C.int64_t(d), C.int64_t(d), C.int64_t(f), (*C.int64_t)(unsafe.Pointer(&sel[0])), &mOut,
+			nil, nil)
+	} else {
+		st = C.bk_multikrum(bkCtx, bkStage, C.BK_HOST_PINNED, C.BK_F64, C.int64_t(n), C.int64_t(d),
+			C.int64_t(d), C.int64_t(f), (*C.int64_t)(unsafe.Pointer(&sel[0])), &mOut, nil, nil)
+	}
 	if st != C.BK_OK {
 		outLog.Printf("Krum failed (%d): %s", int(st), C.GoString(C.bk_last_error()))
 		return []int{}

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 2
+#define BK_ABI_VERSION 3
 
 typedef struct bk_ctx bk_ctx;
 
@@ -119,6 +119,34 @@ int bk_comm_set_mode(bk_ctx *ctx, int deterministic);
 int bk_multikrum_sharded_device(bk_ctx *ctx, const void *dX_local, int dtype, int64_t n,
                                 int64_t d_local, int64_t ld, int64_t f, int64_t *d_sel_idx,
                                 double *d_scores, double *d_mean_local);
+
+/* ---- one process, G GPUs: the Go verifier's form ------
+ * A verifier is ONE process holding [][]float64 in host memory
+ * (VerifyUpdateKRUM, krum.go:227-365).  A group owns one context per device
+ * and splits the columns like bk_multikrum_sharded_device: each device copies
+ * its column shard over its own PCIe link, computes its partial Gram, the
+ * partials are summed, every device scores and selects (identically) and
+ * writes the mean of its columns into mean_out.
+ *   mode BK_GROUP_ALLREDUCE:  ncclAllReduce over one communicator
+ *                             (ncclCommInitAll), devices must be distinct;
+ *   BK_GROUP_DETERMINISTIC:   ncclAllGather + fixed rank-order sum;
+ *   BK_GROUP_HOST_EXCHANGE:   partials through pinned host memory, summed in
+ *                             fixed rank order -- no RCCL; any device list,
+ *                             repeats allowed (bitwise equal to DETERMINISTIC).
+ * devices may be NULL (0..ngpus-1). */
+typedef struct bk_group bk_group;
+enum bk_group_mode { BK_GROUP_ALLREDUCE = 0, BK_GROUP_DETERMINISTIC = 1, BK_GROUP_HOST_EXCHANGE = 2 };
+int bk_group_create(bk_group **out, int ngpus, const int *devices, int mode);
+void bk_group_destroy(bk_group *g);
+int bk_group_size(const bk_group *g);
+/* bk_multikrum's contract (host X: BK_HOST or BK_HOST_PINNED; host outputs;
+ * synchronous) over the group's devices.  shard_bounds: GPU r owns columns
+ * [r*per, min(d, (r+1)*per)), per = ceil(d/G) rounded up to 8. */
+int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t n, int64_t d,
+                       int64_t ld, int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
+                       double *mean_out);
+/* per-device context (timing, streams); r in [0, G) */
+bk_ctx *bk_group_ctx(bk_group *g, int r);
 
 /* ---- synthetic batches (spec: DESIGN.md "Synthetic inputs") --------------
  * Rows [0,n) x columns [c0, c0+d_local) of the n x d_total batch, generated on

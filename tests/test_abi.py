@@ -41,7 +41,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_names():
     L = _lib.lib()
-    assert L.bk_abi_version() == 2
+    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 3
     assert L.bk_kernel_name(0) == b"k_gram"
     assert L.bk_kernel_name(99) == b"?"
     assert len(_lib.KERNELS) == 15
@@ -101,6 +101,16 @@ def test_null_and_bad_arguments_do_not_crash():
     assert L.bk_multikrum(None, None, 0, 0, 10, 10, 10, 2, None, None, None, None) == _lib.BK_EINVAL
     assert L.bk_set_stream(None, None) == _lib.BK_EINVAL
     assert L.bk_timing_read(None, 0, None, None) == _lib.BK_EINVAL
+    assert L.bk_group_create(None, 1, None, 0) == _lib.BK_EINVAL
+    g = ctypes.c_void_p()
+    assert L.bk_group_create(ctypes.byref(g), 0, None, 0) == _lib.BK_EINVAL
+    assert L.bk_group_create(ctypes.byref(g), 2, None, 7) == _lib.BK_EINVAL
+    dup = (ctypes.c_int * 2)(0, 0)  # RCCL modes need distinct devices
+    assert L.bk_group_create(ctypes.byref(g), 2, dup, _lib.BK_GROUP_ALLREDUCE) == _lib.BK_EINVAL
+    assert L.bk_group_multikrum(None, None, 0, 0, 10, 10, 10, 2, None, None, None,
+                                None) == _lib.BK_EINVAL
+    assert L.bk_group_size(None) == 0 and L.bk_group_ctx(None, 0) is None
+    L.bk_group_destroy(None)
 
 
 def test_no_gpu_fails_loudly():
