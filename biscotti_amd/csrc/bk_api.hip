@@ -208,10 +208,11 @@ size_t esize(int dtype) { return dtype == BK_F64 ? 8 : 4; }
 void free_plan(Plan3 &p) {
     if (p.d_groups) (void)hipFree(p.d_groups);
     if (p.d_wg) (void)hipFree(p.d_wg);
+    if (p.d_seg) (void)hipFree(p.d_seg);
     if (p.d_red) (void)hipFree(p.d_red);
     if (p.d_wglist) (void)hipFree(p.d_wglist);
     p.d_groups = nullptr;
-    p.d_wg = p.d_red = p.d_wglist = nullptr;
+    p.d_wg = p.d_red = p.d_wglist = p.d_seg = nullptr;
 }
 
 int get_plan3(bk_ctx *c, int64_t n, int64_t d, int bk, Plan3 **out) {
@@ -229,10 +230,14 @@ int get_plan3(bk_ctx *c, int64_t n, int64_t d, int bk, Plan3 **out) {
     p.T = H.T;
     p.ntile = H.ntile;
     p.ngroups = (int)H.groups.size();
-    p.nwg = (int)H.wg.size() / 5;
+    p.nwg = (int)H.seg.size() / 2;
+    p.nvwg = (int)H.wg.size() / 5;
     p.nfull = H.nfull;
     hipError_t e = hipMalloc(&p.d_groups, H.groups.size() * sizeof(GroupDesc));
     if (e == hipSuccess) e = hipMalloc(&p.d_wg, H.wg.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&p.d_seg, H.seg.size() * sizeof(int));
+    if (e == hipSuccess)
+        e = hipMemcpy(p.d_seg, H.seg.data(), H.seg.size() * sizeof(int), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p.d_red, H.red.size() * sizeof(int));
     if (e == hipSuccess) e = hipMalloc(&p.d_wglist, H.wglist.size() * sizeof(int));
     if (e == hipSuccess)
@@ -276,7 +281,7 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
         pl.d = d;
         pl.T = p3->T;
         pl.ntile = p3->ntile;
-        CHK(ensure(c->part, (size_t)p3->nwg * 16 * 4096 * sizeof(double)));
+        CHK(ensure(c->part, (size_t)p3->nvwg * 16 * 4096 * sizeof(double)));
         double *part = (double *)c->part.p;
         const Plan3 &P3 = *p3;
         long long *trace = nullptr;
@@ -495,7 +500,7 @@ int bk_plan(bk_ctx *c, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *n
     if (S) *S = (int64_t)H.groups.size();
     if (kc) *kc = G3_BK;
     if (ntile) *ntile = H.ntile;
-    if (nwg) *nwg = (int64_t)(H.wg.size() / 5);
+    if (nwg) *nwg = (int64_t)(H.seg.size() / 2);
     return BK_OK;
 }
 

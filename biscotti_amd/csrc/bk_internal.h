@@ -45,7 +45,9 @@ struct Plan3 {
     int n = 0, T = 0, ntile = 0, ngroups = 0, nwg = 0, nfull = 0;
     int64_t d = 0;
     GroupDesc *d_groups = nullptr;  // device copies (owned by the context)
-    int *d_wg = nullptr;            // per workgroup: {group, kstart, kstride, kend, tail}
+    int nvwg = 0;                   // virtual workgroups (segments): one partial slab each
+    int *d_seg = nullptr;           // per launched workgroup: {first segment, segment count}
+    int *d_wg = nullptr;            // per segment: {group, kstart, kstride, kend, tail}
     int *d_red = nullptr;           // per sub-tile u: {list offset, count, slot}
     int *d_wglist = nullptr;        // per group: its workgroups, in reduction order
 };
@@ -54,13 +56,16 @@ struct Plan3 {
 struct Plan3Host {
     int T = 0, ntile = 0, nfull = 0;
     std::vector<GroupDesc> groups;
-    std::vector<int> wg;      // 5 per workgroup
+    std::vector<int> seg;     // 2 per launched workgroup: its segments [v0, v0 + count)
+    std::vector<int> wg;      // 5 per segment (a "virtual workgroup": one group, one slab)
     std::vector<int> red;     // 3 per sub-tile
     std::vector<int> wglist;  // concatenated per-group workgroup lists
 };
 // bk = columns per k-block: 16 for fp64 input, 32 for fp32 (128 B per row either way)
 Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk = G3_BK);
 
+// K1 v3: one launched workgroup runs its segments one after the other (a CU's
+// share of the columns may span two groups: bk_plan.hip "McNaughton")
 hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl,
                         double *part, hipStream_t st, int mode = 0, long long *trace = nullptr);
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st);

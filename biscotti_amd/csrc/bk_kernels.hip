@@ -636,12 +636,12 @@ template <int MODE, typename T = double>
 __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64_t ld, int n,
                                                   int nfull, int64_t d,
                                                   const GroupDesc *__restrict__ groups,
+                                                  const int *__restrict__ segtab,
                                                   const int *__restrict__ wgtab,
                                                   double *__restrict__ part,
                                                   long long *__restrict__ trace) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int *wd = wgtab + 5 * blockIdx.x;
     // debug timeline (BK_TRACE_FILE): per workgroup 100 MHz start/end, shader
     // clock start/end, HW_ID, XCC_ID
     long long t_rt0 = 0, t_mt0 = 0;
@@ -649,20 +649,28 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64
         t_rt0 = (long long)__builtin_amdgcn_s_memrealtime();
         t_mt0 = (long long)__builtin_amdgcn_s_memtime();
     }
-    const GroupDesc &G = groups[wd[0]];
-    double *out = part + ((int64_t)blockIdx.x * 16 + wave * 2) * 4096;
     long long probe[2] = {0, 0};
-    if constexpr (MODE == 0) {
-        switch (G.nb) {
-        case 1: g3_dispatch<T, MODE, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        case 2: g3_dispatch<T, MODE, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        case 3: g3_dispatch<T, MODE, 3>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        case 4: g3_dispatch<T, MODE, 4>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        case 5: g3_dispatch<T, MODE, 5>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-        default: g3_dispatch<T, MODE, 6>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+    const int v0 = segtab[2 * blockIdx.x], nseg = segtab[2 * blockIdx.x + 1];
+    long long ideal = 0;  // sum of nk * cost over the segments (trace only)
+    for (int sg = 0; sg < nseg; ++sg) {
+        const int v = v0 + sg;
+        const int *wd = wgtab + 5 * v;
+        const GroupDesc &G = groups[wd[0]];
+        double *out = part + ((int64_t)v * 16 + wave * 2) * 4096;
+        if (sg > 0) __syncthreads();  // the previous segment's waves are done with the LDS ring
+        if constexpr (MODE == 0) {
+            switch (G.nb) {
+            case 1: g3_dispatch<T, MODE, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+            case 2: g3_dispatch<T, MODE, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+            case 3: g3_dispatch<T, MODE, 3>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+            case 4: g3_dispatch<T, MODE, 4>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+            case 5: g3_dispatch<T, MODE, 5>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+            default: g3_dispatch<T, MODE, 6>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+            }
+        } else {
+            g3_dispatch<T, MODE, 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         }
-    } else {
-        g3_dispatch<T, MODE, 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        if (trace) ideal += (long long)(wd[1] < wd[3] ? (wd[3] - 1 - wd[1]) / wd[2] + 1 : 0) * G.cost;
     }
     if (trace) {
 #ifdef BK_K1_PROBE
@@ -683,8 +691,11 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64
             tr[3] = (long long)__builtin_amdgcn_s_memtime();
             tr[4] = hw;
             tr[5] = xcc;
-            tr[6] = wd[0] | ((long long)G.cost << 32);
-            tr[7] = wd[1] < wd[3] ? (wd[3] - 1 - wd[1]) / wd[2] + 1 : 0;
+            // first segment's group and cost; k-blocks scaled so nk * cost = the ideal
+            const int g0 = nseg > 0 ? wgtab[5 * v0] : 0;
+            const int c0 = groups[g0].cost > 0 ? groups[g0].cost : 1;
+            tr[6] = g0 | ((long long)c0 << 32);
+            tr[7] = (ideal + c0 / 2) / c0;
         }
     }
 }
@@ -1065,16 +1076,16 @@ hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     const dim3 grid((unsigned)pl.nwg), block(512);
     if (dtype != 0)  // fp32 input: production mode only
         hipLaunchKernelGGL((k_gram3<0, float>), grid, block, G3_LDS, st, (const float *)X, ld, n,
-                           pl.nfull, d, pl.d_groups, pl.d_wg, part, trace);
+                           pl.nfull, d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
     else if (mode == 1)
         hipLaunchKernelGGL(k_gram3<1>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
-                           d, pl.d_groups, pl.d_wg, part, trace);
+                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
     else if (mode == 2)
         hipLaunchKernelGGL(k_gram3<2>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
-                           d, pl.d_groups, pl.d_wg, part, trace);
+                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
     else
         hipLaunchKernelGGL(k_gram3<0>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
-                           d, pl.d_groups, pl.d_wg, part, trace);
+                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
     return hipGetLastError();
 }
 

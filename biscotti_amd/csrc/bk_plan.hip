@@ -22,15 +22,16 @@ namespace bk {
 namespace {
 
 constexpr int COST_OFF = 16, COST_PAIR = 20, COST_DIAG1 = 10;
-// measured on MI355X (tools/trace_gram.py): a k-block of a group costs about
-// 256 * cost + 191 * nb shader cycles -- each staged row-block adds ~0.75 cost
-// units of memory stall.  Apportioning by this (not by MFMA cost alone) keeps
-// the column fronts of all groups on an XCD together, so the row-blocks they
-// share are re-read from L2 instead of HBM.
+// Per-k-block time of a group in cost units (256 shader cycles), fitted to the
+// K1 timeline (tools/trace_gram.py, v8 at n = 512, d = 2^20 and 2^17): band
+// quads (cost 36, 4 staged row-blocks) 9730 cycles, super-tile pairs (32, 6)
+// 8880 -> 1.015 * cost + 0.37 * nb.  Only the ratios between groups matter:
+// they set how the planner splits an XCD's columns between groups so that all
+// its CUs finish together.
 double eff_cost(const GroupDesc &g) {
     const char *v = getenv("BK_PLAN_NB_COST");
-    const double a = v ? atof(v) : 0.75;
-    return g.cost + a * g.nb;
+    const double b = v ? atof(v) : 0.37;
+    return 1.015 * g.cost + b * g.nb;
 }
 
 struct Task {
@@ -89,6 +90,58 @@ GroupDesc make_group(int T, const std::vector<Task> &tasks) {
     for (int i = 0; i < G3_MAXB; ++i) G.blk[i] = i < G.nb ? blocks[i] : blocks[0];
     G.cost = group_cost(tasks);
     return G;
+}
+
+// McNaughton's wrap-around rule, one XCD, one dispatch round: the groups'
+// work over a column range of len k-blocks (e[g] per k-block) laid end to end
+// and cut into P equal slot loads; a cut inside a group splits it into two
+// contiguous k-block pieces.  Each slot becomes ONE launched workgroup that
+// runs its pieces as consecutive segments, so the balance does not depend on
+// which CU the dispatcher picks.
+struct Piece {
+    int g;
+    int64_t a, b;  // k-blocks [a, b) relative to the range start
+};
+std::vector<std::vector<Piece>> mcnaughton(const std::vector<double> &e, int64_t len, int P) {
+    std::vector<std::vector<Piece>> slot(P);
+    if (len <= 0) return slot;
+    const int ng = (int)e.size();
+    // the work line: group g occupies [W[g], W[g+1]); cut c sits at c * L.
+    // Each cut is rounded to a k-block boundary on its own (no accumulated
+    // rounding: every slot is within one k-block of L).
+    std::vector<double> W(ng + 1, 0.0);
+    for (int g = 0; g < ng; ++g) W[g + 1] = W[g] + e[g] * (double)len;
+    const double L = W[ng] / P;
+    // cut positions as (group, k-block) pairs, in order
+    std::vector<std::pair<int, int64_t>> cuts;
+    cuts.push_back({0, 0});
+    for (int c = 1; c < P; ++c) {
+        const double pos = c * L;
+        int g = 0;
+        while (g < ng - 1 && W[g + 1] <= pos) ++g;
+        int64_t k = (int64_t)((pos - W[g]) / e[g] + 0.5);
+        k = std::max<int64_t>(0, std::min(len, k));
+        std::pair<int, int64_t> cp{g, k};
+        if (k == len && g < ng - 1) cp = {g + 1, 0};  // a cut at a group's end
+        if (cp < cuts.back()) cp = cuts.back();
+        cuts.push_back(cp);
+    }
+    cuts.push_back({ng - 1, len});
+    for (int q = 0; q < P; ++q) {
+        auto [g0, k0] = cuts[q];
+        const auto [g1, k1] = cuts[q + 1];
+        while (g0 < g1 || (g0 == g1 && k0 < k1)) {
+            const int64_t end = g0 < g1 ? len : k1;
+            if (end > k0) slot[q].push_back({g0, k0, end});
+            if (g0 == g1) break;
+            ++g0;
+            k0 = 0;
+        }
+    }
+    std::vector<std::vector<Piece>> out;
+    for (auto &v : slot)
+        if (!v.empty()) out.push_back(v);
+    return out;
 }
 
 }  // namespace
@@ -185,14 +238,17 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
     // (3) XCD-aware pieces.  Workgroups b and b+8 share an XCD (dispatch is
     //     round-robin; speed only, never correctness).  XCD x owns k-blocks
     //     [K_x, K_x+1), cut into R consecutive sub-ranges, one per dispatch
-    //     round.  In round r group g runs Q_g workgroups, workgroup q taking
-    //     k-blocks K_xr + q, + Q_g, ... < K_x(r+1), so within a round every
-    //     group on an XCD sweeps the same sub-range with its column front
-    //     level with the others', and the row-blocks the groups share are
-    //     re-read from the XCD's L2 instead of HBM.  (Strided over the whole
-    //     XCD range instead, a k-block would be read by one group in round 1
-    //     and by another in round 2: v7 fetched 2x the unique bytes.)
-    //     BK_PLAN_ALIGN=0 restores that v7 interleave for A/B runs.
+    //     round.  BK_PLAN_MODE picks how a round's sub-range is split:
+    //   2 (default for ng <= per_xcd): McNaughton -- the groups' work (eff_cost per k-block)
+    //     laid end to end and cut into per_xcd equal slot loads, each group a
+    //     few contiguous k-block pieces, so every CU of the XCD finishes the
+    //     round together whatever the groups' cost ratios (v8 gave each group
+    //     the same workgroup count, and the cheaper super-tile groups idled
+    //     ~8% of the kernel: fill 0.946);
+    //   1 (default otherwise): v8 -- group g runs Q_g workgroups, workgroup q taking k-blocks
+    //     x_r + q, + Q_g, ... (all groups' column fronts level, for L2 reuse,
+    //     worth < 1%: DESIGN.md);
+    //   0: v7 -- Q_g strided over the whole XCD range.
     const int nfull = H.nfull;
     constexpr int NX = 8;
     const int per_xcd = std::max(1, num_cu / NX);
@@ -204,106 +260,138 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
     const double wg_overhead = ev ? atof(ev) : 100.0;
     const char *er = getenv("BK_PLAN_ROUNDS");
     const int force_rounds = er ? atoi(er) : 0;
-    const char *ea = getenv("BK_PLAN_ALIGN");
-    const bool aligned = ea ? atoi(ea) != 0 : true;
-    double best = 1e300;
-    int bestR = 1;
-    std::vector<int> bestQ(ng, 1);
-    for (int rounds = 1; rounds <= 16; rounds *= 2) {
-        if (force_rounds && rounds != force_rounds) continue;
-        // aligned: Q_g workgroups per round on the XCD's slots; v7: Q_g over
-        // all rounds' slots at once
-        const double slots_total = aligned ? (double)std::max(per_xcd, ng)
-                                           : (double)rounds * per_xcd;
-        if (!aligned && ng > slots_total * 4) continue;
-        // min-max apportionment of the slots (Q_g >= 1): repeatedly give a slot
-        // to the group with the largest eff_g / Q_g.  Equal eff_g / Q_g both
-        // balances the workgroups and makes every group's column front advance
-        // at the same speed (shared row-blocks stay in L2).
-        std::vector<int> Q(ng, 1);
-        {
-            std::priority_queue<std::pair<double, int>> pq;
-            for (int g = 0; g < ng; ++g) pq.push({eff_cost(G[g]), g});
-            for (int used = ng; used < (int)slots_total; ++used) {
-                const int g = pq.top().second;
-                pq.pop();
-                Q[g]++;
-                pq.push({eff_cost(G[g]) / Q[g], g});
-            }
-        }
-        // list-schedule one XCD's workgroups in dispatch order on per_xcd slots
-        std::vector<double> jobs;
-        const int nr = aligned ? rounds : 1;
-        for (int r = 0; r < nr; ++r) {
-            const int64_t R = aligned ? (K[1] - K[0]) * (r + 1) / rounds - (K[1] - K[0]) * r / rounds
-                                      : K[1] - K[0];
-            for (int g = 0; g < ng; ++g)
-                for (int q = 0; q < Q[g]; ++q) {
-                    const int64_t nk = q < R ? (R - 1 - q) / Q[g] + 1 : 0;
-                    jobs.push_back((double)nk * eff_cost(G[g]) + wg_overhead);
+    // McNaughton where an XCD has at least as many CUs as groups (n <= 1024:
+    // D -2.2%, its 8-GPU shard -2.0%, C -0.5% against v8); with more groups
+    // (n = 4096: 256) each slot would run ~8 whole groups back to back, and
+    // v8's one workgroup per group, handed to CUs as they free up, absorbs the
+    // CUs' speed spread better (+3.3% for McNaughton there)
+    int mode = ng <= per_xcd ? 2 : 1;
+    if (const char *em = getenv("BK_PLAN_MODE")) mode = atoi(em);
+    std::vector<double> eg(ng);
+    for (int g = 0; g < ng; ++g) eg[g] = eff_cost(G[g]);
+    auto slab_of = [&](int g) {
+        double b = 0;
+        for (int w = 0; w < 8; ++w)
+            b += G[g].task[w][0] == T_PAIR ? 65536.0 : G[g].task[w][0] != T_NONE ? 32768.0 : 0.0;
+        return b;
+    };
+    // one XCD's launch list for R rounds: launched workgroups, each a list of
+    // segments {group, kstart, kstride, kend, tail}
+    typedef std::array<int, 5> Seg;
+    typedef std::vector<std::vector<std::vector<Seg>>> Lists;
+    auto build_lists = [&](int rounds, Lists &lists) {
+        lists.assign(NX, {});
+        if (mode == 2) {
+            for (int x = 0; x < NX; ++x)
+                for (int r = 0; r < rounds; ++r) {
+                    const int64_t span = K[x + 1] - K[x];
+                    const int64_t k0 = K[x] + span * r / rounds, k1 = K[x] + span * (r + 1) / rounds;
+                    for (const auto &slot : mcnaughton(eg, k1 - k0, per_xcd)) {
+                        std::vector<Seg> wg;
+                        for (const Piece &pc : slot)
+                            wg.push_back({pc.g, (int)(k0 + pc.a), 1, (int)(k0 + pc.b), 0});
+                        lists[x].push_back(wg);
+                    }
                 }
+            return std::vector<int>(ng, 0);
         }
+        // modes 0 / 1: min-max apportionment of slots (Q_g >= 1): repeatedly
+        // give a slot to the group with the largest eff_g / Q_g
+        const double slots_total = mode == 1 ? (double)std::max(per_xcd, ng) : (double)rounds * per_xcd;
+        std::vector<int> Q(ng, 1);
+        std::priority_queue<std::pair<double, int>> pq;
+        for (int g = 0; g < ng; ++g) pq.push({eg[g], g});
+        for (int used = ng; used < (int)slots_total; ++used) {
+            const int g = pq.top().second;
+            pq.pop();
+            Q[g]++;
+            pq.push({eg[g] / Q[g], g});
+        }
+        int maxq = 0;
+        for (int g = 0; g < ng; ++g) maxq = std::max(maxq, Q[g]);
+        const int nr = mode == 1 ? rounds : 1;
+        for (int x = 0; x < NX; ++x)
+            for (int r = 0; r < nr; ++r) {
+                const int64_t span = K[x + 1] - K[x];
+                const int k0 = (int)(K[x] + span * r / nr), k1 = (int)(K[x] + span * (r + 1) / nr);
+                for (int q = 0; q < maxq; ++q)
+                    for (int g = 0; g < ng; ++g)
+                        if (q < Q[g]) lists[x].push_back({Seg{g, k0 + q, Q[g], k1, 0}});
+            }
+        return Q;
+    };
+    auto model = [&](const std::vector<std::vector<Seg>> &l0) {
+        // list-schedule XCD 0's workgroups in dispatch order on per_xcd slots,
+        // + the split-K reduce (K1b) reading every segment's partial slabs
+        // after K1: bytes / ~4 TB/s / (256 cycles at ~2.25 GHz)
         std::priority_queue<double, std::vector<double>, std::greater<double>> slots;
         for (int i = 0; i < per_xcd; ++i) slots.push(0.0);
-        double mk = 0;
-        for (double j : jobs) {
-            const double t1 = slots.top() + j;
+        double mk = 0, slab_bytes = 0;
+        for (const auto &wg : l0) {
+            double t = 0;
+            for (const Seg &e : wg) {
+                const int64_t nk = e[1] < e[3] ? (e[3] - 1 - e[1]) / e[2] + 1 : 0;
+                t += (double)nk * eg[e[0]] + wg_overhead;
+                slab_bytes += slab_of(e[0]) * NX;
+            }
+            const double t1 = slots.top() + t;
             slots.pop();
             slots.push(t1);
             mk = std::max(mk, t1);
         }
-        // + the split-K reduce (K1b) reading every workgroup's partial slabs
-        // after K1, in cost units: bytes / ~4 TB/s / (256 cycles at ~2.25 GHz)
-        double slab_bytes = 0;
-        for (int g = 0; g < ng; ++g) {
-            double b = 0;
-            for (int w = 0; w < 8; ++w)
-                b += G[g].task[w][0] == T_PAIR ? 65536.0 : G[g].task[w][0] != T_NONE ? 32768.0 : 0.0;
-            slab_bytes += b * Q[g] * nr * NX;
-        }
-        mk += slab_bytes / 4e12 / (256.0 / 2.25e9);
+        return mk + slab_bytes / 4e12 / (256.0 / 2.25e9);
+    };
+    double best = 1e300;
+    int bestR = 1;
+    for (int rounds = 1; rounds <= 16; rounds *= 2) {
+        if (force_rounds && rounds != force_rounds) continue;
+        if (mode == 0 && ng > rounds * per_xcd * 4) continue;
+        Lists l;
+        build_lists(rounds, l);
+        const double mk = model(l[0]);
         if (mk < best * 0.995) {
             best = mk;
-            bestQ = Q;
-            bestR = nr;
+            bestR = rounds;
         }
     }
-    // per-XCD launch lists (round-major, then q, then group); b = 8 j + x
-    std::vector<std::vector<std::array<int, 5>>> lists(NX);
-    int maxq = 0;
-    for (int g = 0; g < ng; ++g) maxq = std::max(maxq, bestQ[g]);
-    for (int x = 0; x < NX; ++x)
-        for (int r = 0; r < bestR; ++r) {
-            const int64_t span = K[x + 1] - K[x];
-            const int k0 = (int)(K[x] + span * r / bestR), k1 = (int)(K[x] + span * (r + 1) / bestR);
-            for (int q = 0; q < maxq; ++q)
-                for (int g = 0; g < ng; ++g)
-                    if (q < bestQ[g])
-                        lists[x].push_back({g, k0 + q, bestQ[g], k1,
-                                            (x == 0 && r == 0 && q == 0) ? 1 : 0});
-        }
+    Lists lists;
+    const std::vector<int> bestQ = build_lists(bestR, lists);
+    // exactly one ragged-tail segment per group (XCD 0's first of the group)
+    {
+        std::vector<char> has(ng, 0);
+        for (auto &wg : lists[0])
+            for (auto &e : wg)
+                if (!has[e[0]]) {
+                    has[e[0]] = 1;
+                    e[4] = 1;
+                }
+        for (int g = 0; g < ng; ++g)
+            if (!has[g]) lists[0].push_back({Seg{g, 0, 1, 0, 1}});  // no columns on XCD 0
+    }
+    // launched workgroup b = 8 j + x runs XCD x's j-th list entry; segments
+    // are numbered in launch order (their slabs in part[])
     size_t maxlen = 0;
     for (auto &l : lists) maxlen = std::max(maxlen, l.size());
     std::vector<std::vector<int>> gw(ng);
     for (size_t j = 0; j < maxlen; ++j)
         for (int x = 0; x < NX; ++x) {
-            const int b = (int)(H.wg.size() / 5);
-            if (j < lists[x].size()) {
-                const auto &e = lists[x][j];
-                H.wg.insert(H.wg.end(), e.begin(), e.end());
-                gw[e[0]].push_back(b);
-            } else {
-                // keep b = 8j + x: an empty workgroup (no k-blocks) of group 0
-                H.wg.insert(H.wg.end(), {0, 0, 1, 0, 0});
-                gw[0].push_back(b);
-            }
+            const int v0 = (int)(H.wg.size() / 5);
+            int cnt = 0;
+            if (j < lists[x].size())
+                for (const Seg &e : lists[x][j]) {
+                    gw[e[0]].push_back((int)(H.wg.size() / 5));
+                    H.wg.insert(H.wg.end(), e.begin(), e.end());
+                    ++cnt;
+                }
+            H.seg.push_back(v0);
+            H.seg.push_back(cnt);  // 0: an idle workgroup keeps b = 8 j + x
         }
     for (int g = 0; g < ng; ++g) {
-        G[g].Q = bestQ[g] * bestR;
+        G[g].Q = mode == 2 ? 0 : bestQ[g] * (mode == 1 ? bestR : 1);
         G[g].wg0 = (int)H.wglist.size();
         H.wglist.insert(H.wglist.end(), gw[g].begin(), gw[g].end());
     }
-    // every (group, k-block) exactly once, and exactly one tail workgroup per group
+    // every (group, k-block) exactly once, and exactly one tail segment per group
     bool covered = true;
     {
         std::vector<int> seen((size_t)ng * nfull, 0), tails(ng, 0);
