@@ -295,3 +295,36 @@ def test_nan_and_inf_rows(engine, oracle):
         np.testing.assert_array_equal(np.isnan(sc), np.isnan(osc))
         fin = np.isfinite(osc)
         np.testing.assert_allclose(sc[fin], osc[fin], rtol=1e-12, atol=0)
+
+
+def test_concurrent_callers_one_context_and_two(oracle):
+    """The Go verifier calls from goroutines on arbitrary OS threads
+    (krum.go:194,284 serialise Krum with krumLock, but the miner-side calls
+    do not): 6 Python threads share one context, 2 more use a second context
+    on the same device; every result must equal the oracle's."""
+    import threading
+    from biscotti_amd.krum import Engine
+    cases = [(60 + 7 * i, 400 + 33 * i, 10 + i) for i in range(8)]
+    data = [oracle.synth(n, d, 500 + i, f) for i, (n, d, f) in enumerate(cases)]
+    want = [oracle.krum(X, f) for X, (n, d, f) in zip(data, cases)]
+    e1, e2 = Engine(0), Engine(0)
+    errors = []
+
+    def run(i, eng):
+        try:
+            for _ in range(3):
+                sel, sc, mean = eng.multikrum(data[i], cases[i][2])
+                assert np.array_equal(sel, want[i][0])
+                scale = float(np.max(np.mean(np.abs(data[i][want[i][0]]), axis=0)))
+                assert float(np.max(np.abs(mean - want[i][2]))) <= 1e-9 * scale
+        except Exception as ex:  # surfaced below
+            errors.append((i, repr(ex)))
+
+    ts = [threading.Thread(target=run, args=(i, e1 if i < 6 else e2)) for i in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    e1.close()
+    e2.close()
+    assert not errors, errors
