@@ -472,8 +472,11 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
         const int64_t col = kb * BKE;
         char *base = lds + stage * G3_STAGE;
 #pragma unroll
+#ifndef BK_K1_GLDS_LIMIT  // timing-only ablation: issue at most this many glds per wave
+#define BK_K1_GLDS_LIMIT G3_MAXB
+#endif
         for (int m = 0; m < (NB > 0 ? NB : G3_MAXB); ++m)
-            if (NB > 0 || m < c)
+            if ((NB > 0 || m < c) && m < BK_K1_GLDS_LIMIT)
                 __builtin_amdgcn_global_load_lds((const void *)(gsrc[m] + col),
                                                  (void *)(base + gdst[m]), 16, 0, 0);
     };
@@ -504,7 +507,7 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
         G3_PROBE(p0);
         if constexpr (NB > 0 && MODE != 2) {
             if (ahead > 0)
-                g3_waitc<NB>();
+                g3_waitc<(NB < BK_K1_GLDS_LIMIT ? NB : BK_K1_GLDS_LIMIT)>();
             else
                 g3_waitc<0>();
         } else {
