@@ -527,13 +527,15 @@ int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
     const void *dX = X;
     int64_t dld = ld;
     if (where != BK_DEVICE) {
-        CHK(ensure(c->X, (size_t)n * d * es));
-        dld = d;
+        // device rows padded to 16 B so K1 v3 (global_load_lds granules) always applies
+        const int64_t epg = (int64_t)(16 / es);
+        dld = (d + epg - 1) / epg * epg;
+        CHK(ensure(c->X, (size_t)n * dld * es));
         void *dst = c->X.p;
         CHK(timed(c, BK_K_H2D, [&] {
-            if (ld == d) return hipMemcpyAsync(dst, X, (size_t)n * d * es, hipMemcpyHostToDevice,
-                                               c->stream);
-            return hipMemcpy2DAsync(dst, (size_t)d * es, X, (size_t)ld * es, (size_t)d * es,
+            if (ld == d && dld == d)
+                return hipMemcpyAsync(dst, X, (size_t)n * d * es, hipMemcpyHostToDevice, c->stream);
+            return hipMemcpy2DAsync(dst, (size_t)dld * es, X, (size_t)ld * es, (size_t)d * es,
                                     (size_t)n, hipMemcpyHostToDevice, c->stream);
         }));
         dX = dst;
