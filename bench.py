@@ -162,6 +162,57 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
     return res
 
 
+def graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt):
+    """bk_graph_enable: the same device-resident step eager vs replayed as one
+    hipGraph (no per-kernel events in either), on the headline batch and on the
+    launch-bound config B (100 x 7,850)."""
+    import torch
+    from biscotti_amd import _lib
+
+    def timed(fn, steps):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    wb = WORKLOADS["B_mnist"]
+    nb, db, fb = wb["n"], wb["d"], wb["f"]
+    Xb = torch.empty((nb, db), dtype=torch.float64, device=dev)
+    eng.synth_fill_ptr(Xb.data_ptr(), _lib.BK_F64, nb, db, db, 0, db, wb["seed"], wb["nbyz"],
+                       flags=wb.get("flags", 0))
+    selb = torch.empty(nb - fb, dtype=torch.int64, device=dev)
+    scb = torch.empty(nb, dtype=torch.float64, device=dev)
+    mb = torch.empty(db, dtype=torch.float64, device=dev)
+    cases = {
+        "B_100x7850": (lambda: eng.multikrum_device_ptr(Xb.data_ptr(), _lib.BK_F64, nb, db, db, fb,
+                                                        selb.data_ptr(), scb.data_ptr(),
+                                                        mb.data_ptr()), 300, nb * db * 8,
+                       (selb, mb)),
+        "D_512x1M_f153": (lambda: eng.multikrum_device_ptr(X.data_ptr(), bdt, n, d, X.stride(0), f,
+                                                           sel.data_ptr(), scores.data_ptr(),
+                                                           mean.data_ptr()), 10,
+                          n * d * X.element_size(), (sel, mean)),
+    }
+    res = {}
+    eng.timing_enable(False)
+    for name, (fn, steps, nbytes, outs) in cases.items():
+        eng.graph_enable(False)
+        t_eager = timed(fn, steps)
+        ref = [o.clone() for o in outs]
+        eng.graph_enable(True)
+        t_graph = timed(fn, steps)
+        same = all(torch.equal(o, r) for o, r in zip(outs, ref))
+        eng.graph_enable(False)
+        res[name] = {"eager_ms": round(t_eager, 4), "graph_ms": round(t_graph, 4),
+                     "graph_GB_per_s": round(nbytes / (t_graph * 1e-3) / 1e9, 2),
+                     "bitwise_same": bool(same)}
+    return res
+
+
 def golden_check(name, sel_host, mean_local, c0, dl):
     path = os.path.join(REPO, "tests", "golden", name + ".npz")
     if not os.path.exists(path):
@@ -366,6 +417,9 @@ def main():
 
     if rank == 0 and world == 1 and not emu and not a.no_next_rows and w["dtype"] == "f64":
         out["next_rows"] = next_rows(eng, X, n, d, sel, m)
+
+    if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD:
+        out["hip_graph"] = graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt)
 
     if rank == 0 and world == 1 and not emu and not a.no_e2e:
         # PCIe-inclusive rate: pinned host batch -> H2D -> Multi-Krum -> D2H of sel and mean

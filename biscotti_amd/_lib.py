@@ -16,7 +16,7 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
-BK_ABI_VERSION = 3
+BK_ABI_VERSION = 4
 KERNELS = ["k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni"]
 K = {name: i for i, name in enumerate(KERNELS)}
@@ -52,6 +52,7 @@ SIGNATURES = {
     "bk_synth_fill_device": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _i64, _u64, _i64, _d, _d,
                                   _d, _i]),
     "bk_timing_enable": (_i, [_p, _i]),
+    "bk_graph_enable": (_i, [_p, _i]),
     "bk_timing_select": (_i, [_p, ctypes.c_uint32]),
     "bk_timing_read": (_i, [_p, _i, _pd, _pi64]),
     "bk_kernel_name": (ctypes.c_char_p, [_i]),

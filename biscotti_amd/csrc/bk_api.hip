@@ -65,6 +65,7 @@ const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_expand"
 struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
+    uint64_t *epoch = nullptr;  // the owning context's ws_epoch (graph invalidation)
 };
 
 }  // namespace
@@ -102,6 +103,22 @@ struct bk_ctx {
     std::vector<CachedPlan> plans;
     int gram_variant = 3;  // 3: LDS-shared v3 for aligned fp64; 1: v1 everywhere (BK_GRAM=v1)
     int gram_mode = 0;     // BK_GRAM_MODE: timing-only ablations of v3 (tools/, never tests)
+    // hipGraph replay of bk_multikrum_device (bk_graph_enable): one captured
+    // launch sequence per call signature; every workspace reallocation or plan
+    // eviction bumps ws_epoch, which retires the graphs that baked the old
+    // pointers in
+    int graph_on = 0;
+    uint64_t ws_epoch = 0;
+    struct CachedGraph {
+        const void *X;
+        int dtype;
+        int64_t n, d, ld, f;
+        const void *sel, *scores, *mean;
+        uint64_t epoch;
+        hipGraph_t g;
+        hipGraphExec_t exec;
+    };
+    std::vector<CachedGraph> graphs;
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -112,6 +129,7 @@ namespace {
 
 int ensure(DevBuf &b, size_t bytes) {
     if (bytes <= b.bytes) return BK_OK;
+    if (b.epoch) ++*b.epoch;  // pointers baked into captured graphs are about to change
     if (b.p) {
         hipError_t e = hipFree(b.p);
         b.p = nullptr;
@@ -126,6 +144,21 @@ int ensure(DevBuf &b, size_t bytes) {
     }
     b.bytes = want;
     return BK_OK;
+}
+
+void drop_graph(bk_ctx::CachedGraph &cg) {
+    if (cg.exec) (void)hipGraphExecDestroy(cg.exec);
+    if (cg.g) (void)hipGraphDestroy(cg.g);
+    cg.exec = nullptr;
+    cg.g = nullptr;
+}
+
+// every workspace buffer of c bumps c->ws_epoch when it is reallocated
+void bind_epoch(bk_ctx *c) {
+    DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,   &c->scores, &c->mask,   &c->sel,
+                      &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
+                      &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s};
+    for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
 int get_event(bk_ctx *c, hipEvent_t *out) {
@@ -257,6 +290,7 @@ int get_plan3(bk_ctx *c, int64_t n, int64_t d, int bk, Plan3 **out) {
     if (c->plans.size() >= 8) {
         free_plan(c->plans.front().p);
         c->plans.erase(c->plans.begin());
+        ++c->ws_epoch;  // a captured graph may point at the evicted tables
     }
     c->plans.push_back({(int)n, d, bk, p});
     *out = &c->plans.back().p;
@@ -398,6 +432,7 @@ int bk_create(bk_ctx **out, int device) {
     bk_ctx *c = new (std::nothrow) bk_ctx();
     if (!c) return fail(BK_ENOMEM, "host allocation of bk_ctx failed");
     c->device = device;
+    bind_epoch(c);
     DeviceGuard dg(device);
     hipDeviceProp_t prop;
     hipError_t e = hipGetDeviceProperties(&prop, device);
@@ -440,6 +475,7 @@ void bk_destroy(bk_ctx *c) {
         }
         for (hipEvent_t ev : c->pool) (void)hipEventDestroy(ev);
         for (auto &cp : c->plans) free_plan(cp.p);
+        for (auto &cg : c->graphs) drop_graph(cg);
         if (c->comm) (void)ncclCommDestroy(c->comm);
         if (c->own) (void)hipStreamDestroy(c->own);
     }
@@ -504,6 +540,62 @@ int bk_plan(bk_ctx *c, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *n
     return BK_OK;
 }
 
+namespace {
+
+// The 7-launch step (K1, K1b, K2, K3, K3b, K4) replayed as one hipGraph: the
+// first call of a signature runs eagerly (allocating workspace and the K1
+// plan), the second captures the same sequence, later ones replay it.  Only
+// without per-kernel timing (events are not captured).
+int run_device_graph(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
+                     int64_t f, int64_t *d_sel, double *d_scores, double *d_mean) {
+    for (size_t i = 0; i < c->graphs.size();) {  // retire graphs over stale workspace
+        if (c->graphs[i].epoch != c->ws_epoch) {
+            drop_graph(c->graphs[i]);
+            c->graphs.erase(c->graphs.begin() + i);
+        } else {
+            ++i;
+        }
+    }
+    for (auto &cg : c->graphs)
+        if (cg.X == dX && cg.dtype == dtype && cg.n == n && cg.d == d && cg.ld == ld && cg.f == f &&
+            cg.sel == d_sel && cg.scores == d_scores && cg.mean == d_mean) {
+            HIPCHK(hipGraphLaunch(cg.exec, c->stream));
+            return BK_OK;
+        }
+    // eager run first: every ensure() / plan build happens outside the capture
+    const uint64_t e0 = c->ws_epoch;
+    CHK(run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean));
+    if (c->ws_epoch != e0) return BK_OK;  // workspace moved: capture on the next call
+    bk_ctx::CachedGraph cg{dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean, c->ws_epoch, nullptr,
+                           nullptr};
+    HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    const int st = run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
+    hipGraph_t g = nullptr;
+    const hipError_t ee = hipStreamEndCapture(c->stream, &g);
+    if (st != BK_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return st;
+    }
+    if (ee != hipSuccess) return fail(BK_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(ee));
+    cg.g = g;
+    const hipError_t ei = hipGraphInstantiate(&cg.exec, g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+        drop_graph(cg);
+        return fail(BK_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+    }
+    if (c->ws_epoch != e0) {  // cannot happen after an eager run of the same call; be safe
+        drop_graph(cg);
+        return BK_OK;
+    }
+    if (c->graphs.size() >= 4) {
+        drop_graph(c->graphs.front());
+        c->graphs.erase(c->graphs.begin());
+    }
+    c->graphs.push_back(cg);
+    return BK_OK;  // the captured run is not executed: the eager one produced this call's outputs
+}
+}  // namespace
+
 int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
                         int64_t f, int64_t *d_sel, double *d_scores, double *d_mean) {
     CHK(check_common(c, dX, dtype, n, d, ld));
@@ -511,7 +603,21 @@ int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t
     if (!d_sel) return fail(BK_EINVAL, "null d_sel_idx");
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
+    if (c->graph_on && c->timing == 0 && !getenv("BK_TRACE_FILE"))
+        return run_device_graph(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
     return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
+}
+
+int bk_graph_enable(bk_ctx *c, int on) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    c->graph_on = on ? 1 : 0;
+    if (!on) {
+        for (auto &cg : c->graphs) drop_graph(cg);
+        c->graphs.clear();
+    }
+    return BK_OK;
 }
 
 int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int64_t d, int64_t ld,

@@ -228,6 +228,10 @@ class Engine:
     def timing_enable(self, on=True):
         check(lib().bk_timing_enable(self._ctx, 1 if on else 0))
 
+    def graph_enable(self, on=True):
+        """Replay multikrum_device_ptr calls as hipGraphs (bk_graph_enable)."""
+        check(lib().bk_graph_enable(self._ctx, 1 if on else 0))
+
     def timing_select(self, kernels):
         """Time only these kernels (names from _lib.KERNELS)."""
         mask = 0

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 3
+#define BK_ABI_VERSION 4
 
 typedef struct bk_ctx bk_ctx;
 
@@ -94,6 +94,12 @@ int bk_multikrum(bk_ctx *ctx, const void *X, int where, int dtype, int64_t n, in
 int bk_multikrum_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
                         int64_t ld, int64_t f, int64_t *d_sel_idx, double *d_scores,
                         double *d_mean);
+/* Replay bk_multikrum_device as a hipGraph (one captured launch sequence per
+ * call signature: pointers, shape, f; up to 4 cached).  The first call of a
+ * signature runs eagerly, the second captures, later ones replay; graphs are
+ * bypassed while per-kernel timing is on, and retired when the context's
+ * workspace is reallocated.  Off by default; on = 0 frees the cached graphs. */
+int bk_graph_enable(bk_ctx *ctx, int on);
 
 /* ---- dimension-sharded stages (one process / device per column shard) ----
  * Packed upper-triangle Gram: bk_upper_elems(n) doubles.  Summing the packed
