@@ -398,6 +398,26 @@ def main():
             "kernel": "k_gram", "kernel_avg_ms": round(g["avg_ms"], 4),
             "flops_per_launch": flops}
 
+    # the whole step against its floor: t_floor = max(flops_alg / fp64
+    # matrix peak, bytes_alg / HBM peak) with bytes_alg = (n + m) * d_local * s + 8 d_local;
+    # and K4 (k_mean, the HBM-bound kernel) against HBM: m * d_local * s + 8 d_local bytes
+    bytes_alg = (n + m) * dl * es + 8 * dl
+    t_mfma = flops / (peak * 1e12) * 1e3
+    t_hbm = bytes_alg / (PEAK_HBM_GBS * 1e9) * 1e3
+    step_roof = {"t_floor_ms": round(max(t_mfma, t_hbm), 4),
+                 "bound": "mfma" if t_mfma >= t_hbm else "hbm",
+                 "t_measured_ms": round(ms_per_step, 4),
+                 "frac": round(max(t_mfma, t_hbm) / ms_per_step, 4)}
+    km = kbreak.get("k_mean")
+    if km:
+        kb = m * dl * es + 8 * dl
+        kgbs = kb / (km["avg_ms"] * 1e-3) / 1e9
+        k4_roof = {"bound": "hbm", "achieved": round(kgbs, 1), "peak": PEAK_HBM_GBS,
+                   "unit": "GB/s", "frac": round(kgbs / PEAK_HBM_GBS, 4), "kernel": "k_mean",
+                   "kernel_avg_ms": round(km["avg_ms"], 4), "bytes_per_launch": kb}
+    else:
+        k4_roof = None
+
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -409,6 +429,8 @@ def main():
                    ("emulated rank 0 of %d (1 GPU)" % emu if emu else "1 GPU"),
                    "d_local": dl},
         "roofline": roof,
+        "roofline_hbm_k4": k4_roof,
+        "step_roofline": step_roof,
         "kernels_ms_avg": {k: round(v["avg_ms"], 5) for k, v in kbreak.items()},
         "parity": parity,
     }
