@@ -132,6 +132,35 @@ def test_misaligned_device_pointer(engine, oracle):
     assert np.max(np.abs(mean - omean)) <= 1e-9 * np.max(np.abs(omean)) * 10
 
 
+def test_odd_ld_device_rows(engine, oracle):
+    """Device rows whose starts are not all 16-B aligned (odd ld): the
+    direct-to-register K1 (k_gram v1).  Host input is re-staged with a padded
+    ld and never takes this path."""
+    n, d, f, ld = 90, 1003, 27, 1005
+    X = oracle.synth(n, d, 6, f)
+    buf = torch.zeros((n, ld), dtype=torch.float64, device="cuda")
+    buf[:, :d] = torch.from_numpy(X).cuda()
+    sel, sc, mean = _dev_run(engine, buf[:, :d], f)
+    osel, osc, omean = oracle.krum(X, f)
+    assert np.array_equal(sel, osel)
+    assert np.max(np.abs(sc - osc)) <= 1e-9 * np.max(np.abs(osc))
+    mscale = np.max(np.mean(np.abs(X[osel]), axis=0))
+    assert np.max(np.abs(mean - omean)) <= 1e-9 * mscale
+
+
+@pytest.mark.parametrize("n,d,f", [(16384, 40, 4915), (9001, 33, 1)])
+def test_max_n(engine, oracle, n, d, f):
+    """BK_MAX_N = 16384 updates (the row sort takes 128 KiB of LDS), and a
+    ragged n just past 9000 with k = n - 3."""
+    X = oracle.synth(n, d, 7 + n, f)
+    sel, sc, mean = engine.multikrum(X, f)
+    osel, osc, omean = oracle.krum(X, f)
+    assert np.array_equal(sel, osel)
+    assert np.max(np.abs(sc - osc)) <= 1e-9 * np.max(np.abs(osc))
+    mscale = np.max(np.mean(np.abs(X[osel]), axis=0))
+    assert np.max(np.abs(mean - omean)) <= 1e-9 * mscale
+
+
 def test_deterministic_bitwise(engine):
     n, d, f = 512, 200003, 153
     X = torch.empty((n, d), dtype=torch.float64, device="cuda")
