@@ -39,6 +39,12 @@ struct GroupDesc {
     int wg0;              // offset of this group's list in wglist
     int cost;             // max over SIMDs of its two waves' MFMA units per k-step
     int task[8][5];       // per wave: {kind, slotA, slotB, u0, u1}
+    // balanced band quads (bk_plan.hip): block (0,3) of each diagonal tile moves
+    // from the PAIR wave to a super-tile OFF wave holding that row-block.
+    // xt: PAIR 1 = skip block (0,3); OFF 1 / 2 = also compute block (0,3) of the
+    // diagonal tile of its A / B row-block, into slab slot xslot (the PAIR's)
+    int xt[8];
+    int xslot[8];
 };
 
 struct Plan3 {

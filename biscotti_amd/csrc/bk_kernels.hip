@@ -332,17 +332,21 @@ struct G3Acc<T_DIAG1> {
     d4v a[10];
 };
 
+// SKIP: leave block (0,3) to the OFF wave that took it (balanced band quads)
+template <bool SKIP = false>
 __device__ __forceinline__ void diag_mma(d4v (&acc)[10], const d2v (&a)[4]) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = i; j < 4; ++j)
+            for (int j = i; j < 4; ++j) {
+                if (SKIP && i == 0 && j == 3) continue;
                 acc[dix(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][s], a[j][s], acc[dix(i, j)], 0, 0, 0);
+            }
 }
 // the same over one granule of either input type
-template <typename T>
+template <typename T, bool SKIP = false>
 __device__ __forceinline__ void diag_mma_g(d4v (&acc)[10], const typename G3T<T>::gran (&a)[4]) {
 #pragma unroll
     for (int s = 0; s < G3T<T>::SUB; ++s) {
@@ -352,8 +356,10 @@ __device__ __forceinline__ void diag_mma_g(d4v (&acc)[10], const typename G3T<T>
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = i; j < 4; ++j)
+            for (int j = i; j < 4; ++j) {
+                if (SKIP && i == 0 && j == 3) continue;
                 acc[dix(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[i], v[j], acc[dix(i, j)], 0, 0, 0);
+            }
     }
 }
 
@@ -378,20 +384,25 @@ __device__ __forceinline__ void store_tile(double *out, const d4v (&acc)[4][4], 
             for (int r = 0; r < 4; ++r) out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = acc[i][j][r];
 }
 
+template <bool SKIP = false>
 __device__ __forceinline__ void store_diag(double *out, const d4v (&acc)[10], int rr, int g) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+            if (SKIP && i == 0 && j == 3) continue;  // written by the OFF wave that took it
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = j >= i ? acc[dix(i, j)][r] : 0.0;
+        }
 }
 
-// one MFMA sub-step S (element S of each lane's granule) of an off-diagonal tile
-template <typename T, int S>
+// one MFMA sub-step S (element S of each lane's granule) of an off-diagonal
+// tile; XT = 1 / 2: also block (0,3) of the diagonal tile of the A / B row-block
+// (operands already in registers: fragments 0 and 3 of that side)
+template <typename T, int S, int XT = 0>
 __device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const typename G3T<T>::gran (&a)[4],
-                                        const typename G3T<T>::gran (&b)[4]) {
+                                        const typename G3T<T>::gran (&b)[4], d4v &x) {
     double va[4], vb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -403,16 +414,18 @@ __device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const typename G3T<T>:
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[i], vb[j], acc[i][j], 0, 0, 0);
+    if constexpr (XT == 1) x = __builtin_amdgcn_mfma_f64_16x16x4f64(va[0], va[3], x, 0, 0, 0);
+    if constexpr (XT == 2) x = __builtin_amdgcn_mfma_f64_16x16x4f64(vb[0], vb[3], x, 0, 0, 0);
 }
 // all SUB sub-steps of one granule
-template <typename T>
+template <typename T, int XT = 0>
 __device__ __forceinline__ void off_mma_gran(d4v (&acc)[4][4], const typename G3T<T>::gran (&a)[4],
-                                             const typename G3T<T>::gran (&b)[4]) {
-    off_mma<T, 0>(acc, a, b);
-    off_mma<T, 1>(acc, a, b);
+                                             const typename G3T<T>::gran (&b)[4], d4v &x) {
+    off_mma<T, 0, XT>(acc, a, b, x);
+    off_mma<T, 1, XT>(acc, a, b, x);
     if constexpr (G3T<T>::SUB == 4) {
-        off_mma<T, 2>(acc, a, b);
-        off_mma<T, 3>(acc, a, b);
+        off_mma<T, 2, XT>(acc, a, b, x);
+        off_mma<T, 3, XT>(acc, a, b, x);
     }
 }
 // STAG: waves 4-7 (the SIMD partners of waves 0-3) run their OFF tile half a
@@ -430,10 +443,16 @@ __device__ __forceinline__ void off_mma_gran(d4v (&acc)[4][4], const typename G3
 #endif
 // NB > 0: the group stages exactly NB row-blocks (compile time: a single
 // s_waitcnt and straight-line glds); NB = 0: read G.nb at run time.
-template <typename T, int KIND, int MODE, bool STAG, int NB>
+// XT (balanced band quads, GroupDesc::xt): OFF 1 / 2 = also block (0,3) of the
+// A / B row-block's diagonal tile, stored into xout (the PAIR wave's slab);
+// PAIR 1 = skip that block in both diagonal tiles
+template <typename T, int KIND, int MODE, bool STAG, int NB, int XT = 0>
 __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int n, int nfull,
                                         int64_t d, const GroupDesc &G, const int *wd, char *lds,
-                                        int wave, int lane, double *out, long long (&probe)[2]) {
+                                        int wave, int lane, double *out, long long (&probe)[2],
+                                        double *xout = nullptr) {
+    constexpr int XO = KIND == T_OFF ? XT : 0;     // OFF: extra block side
+    constexpr bool XP = KIND == T_PAIR && XT != 0;  // PAIR: skip block (0,3)
     typedef typename G3T<T>::gran gran;
     constexpr int EPG = 16 / (int)sizeof(T);  // elements per 16-B granule
     constexpr int BKE = 8 * EPG;               // columns per k-block (16 fp64, 32 fp32)
@@ -494,6 +513,7 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
 #pragma unroll
         for (int i = 0; i < 10; ++i) acc.a[i] = d4v{0.0, 0.0, 0.0, 0.0};
     }
+    d4v xacc = d4v{0.0, 0.0, 0.0, 0.0};  // XO: the extra diagonal block
     gran ha[4], hb[4];  // STAG: the held second granule of the previous k-block
 #pragma unroll
     for (int q = 0; q < 4; ++q) ha[q] = hb[q] = gran{};
@@ -534,14 +554,14 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
 #pragma unroll
             for (int q = 0; q < 4; ++q) b0[q] = g3_frag<T>(ls + sB * G3_BLK, q, 0, rr, g);
             if constexpr (STAG) {
-                if (t > 0) off_mma_gran<T>(acc.a, ha, hb);
+                if (t > 0) off_mma_gran<T, XO>(acc.a, ha, hb, xacc);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) a1[q] = g3_frag<T>(ls + sA * G3_BLK, q, 1, rr, g);
 #pragma unroll
             for (int q = 0; q < 4; ++q) b1[q] = g3_frag<T>(ls + sB * G3_BLK, q, 1, rr, g);
             if (more) issue(nkb, nbuf);
-            off_mma_gran<T>(acc.a, a0, b0);
+            off_mma_gran<T, XO>(acc.a, a0, b0, xacc);
             if constexpr (STAG) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -549,7 +569,7 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
                     hb[q] = b1[q];
                 }
             } else {
-                off_mma_gran<T>(acc.a, a1, b1);
+                off_mma_gran<T, XO>(acc.a, a1, b1, xacc);
             }
         } else if constexpr (KIND == T_PAIR) {
 #pragma unroll
@@ -560,8 +580,8 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
 #pragma unroll
                 for (int q = 0; q < 4; ++q) b[q] = g3_frag<T>(ls + sB * G3_BLK, q, h, rr, g);
                 if (h == 0 && more) issue(nkb, nbuf);
-                diag_mma_g<T>(acc.a, a);
-                diag_mma_g<T>(acc.b, b);
+                diag_mma_g<T, XP>(acc.a, a);
+                diag_mma_g<T, XP>(acc.b, b);
             }
         } else if constexpr (KIND == T_DIAG1) {
 #pragma unroll
@@ -577,7 +597,7 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
         }
     }
     if constexpr (KIND == T_OFF && STAG && MODE != 1)
-        if (nk > 0) off_mma_gran<T>(acc.a, ha, hb);
+        if (nk > 0) off_mma_gran<T, XO>(acc.a, ha, hb, xacc);
     if constexpr (KIND != T_NONE) {
         // ragged tail columns [nfull*BKE, d): one workgroup per group, direct loads
         const int64_t c0 = (int64_t)nfull * BKE;
@@ -590,9 +610,16 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
                 g3_load_rows<T>(b, X, ld, n, blk[sB], cc, d, rr);
                 if constexpr (KIND == T_OFF) {
                     gram_mma<false>(acc.a, a, b);
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        if constexpr (XO == 1)
+                            xacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0][s2], a[3][s2], xacc, 0, 0, 0);
+                        if constexpr (XO == 2)
+                            xacc = __builtin_amdgcn_mfma_f64_16x16x4f64(b[0][s2], b[3][s2], xacc, 0, 0, 0);
+                    }
                 } else if constexpr (KIND == T_PAIR) {
-                    diag_mma(acc.a, a);
-                    diag_mma(acc.b, b);
+                    diag_mma<XP>(acc.a, a);
+                    diag_mma<XP>(acc.b, b);
                 } else {
                     diag_mma(acc.a, a);
                 }
@@ -600,9 +627,13 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
         }
         if constexpr (KIND == T_OFF) {
             store_tile(out, acc.a, rr, g);
+            if constexpr (XO != 0) {  // block (0,3) of the PAIR wave's diagonal tile
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xout[(g + 4 * r) * 64 + 48 + rr] = xacc[r];
+            }
         } else if constexpr (KIND == T_PAIR) {
-            store_diag(out, acc.a, rr, g);
-            store_diag(out + 4096, acc.b, rr, g);
+            store_diag<XP>(out, acc.a, rr, g);
+            store_diag<XP>(out + 4096, acc.b, rr, g);
         } else {
             store_diag(out, acc.a, rr, g);
         }
@@ -617,15 +648,31 @@ __device__ __forceinline__ void g3_dispatch(const T *__restrict__ X, int64_t ld,
                                             int nfull, int64_t d, const GroupDesc &G,
                                             const int *wd, char *lds, int wave, int lane,
                                             double *out, long long (&probe)[2]) {
+    const int xt = G.xt[wave];
+    double *xout = out - (int64_t)wave * 2 * 4096 + (int64_t)G.xslot[wave] * 4096;
     switch (G.task[wave][0]) {
     case T_OFF:
-        if (wave >= 4 && G3_STAGGER)
-            g3_wave<T, T_OFF, MODE, true, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
-        else
-            g3_wave<T, T_OFF, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        if (wave >= 4 && G3_STAGGER) {
+            if (xt == 1)
+                g3_wave<T, T_OFF, MODE, true, NB, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+            else if (xt == 2)
+                g3_wave<T, T_OFF, MODE, true, NB, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+            else
+                g3_wave<T, T_OFF, MODE, true, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        } else {
+            if (xt == 1)
+                g3_wave<T, T_OFF, MODE, false, NB, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+            else if (xt == 2)
+                g3_wave<T, T_OFF, MODE, false, NB, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+            else
+                g3_wave<T, T_OFF, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        }
         break;
     case T_PAIR:
-        g3_wave<T, T_PAIR, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        if (xt)
+            g3_wave<T, T_PAIR, MODE, false, NB, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        else
+            g3_wave<T, T_PAIR, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         break;
     case T_DIAG1:
         g3_wave<T, T_DIAG1, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);

@@ -38,6 +38,7 @@ struct Task {
     int kind;
     int ba, bb;  // row-blocks (OFF: bi, bj; PAIR: b0, b1; DIAG1: b0, b0)
     int cost;
+    int xt = 0, xslot = -1;  // balanced band quads (GroupDesc::xt)
 };
 
 int upper_index(int T, int bi, int bj) { return bi * T - bi * (bi - 1) / 2 + (bj - bi); }
@@ -67,6 +68,8 @@ GroupDesc make_group(int T, const std::vector<Task> &tasks) {
         return (int)blocks.size() - 1;
     };
     for (int w = 0; w < 8; ++w) {
+        G.xt[w] = w < (int)tasks.size() ? tasks[w].xt : 0;
+        G.xslot[w] = w < (int)tasks.size() ? tasks[w].xslot : -1;
         int *t = G.task[w];
         t[0] = T_NONE;
         t[1] = t[2] = 0;
@@ -186,6 +189,26 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
         const std::vector<Task> st = super_tasks(I, I + 1);
         const int slots[4] = {2, 3, 6, 7};
         for (size_t k = 0; k < st.size(); ++k) w[slots[k]] = st[k];
+        // Balance: the quad's 136 MFMA units sit 20 + 16 on SIMDs 0-1 and
+        // 16 + 16 on SIMDs 2-3.  Block (0,3) of each of the four diagonal tiles
+        // (1 unit) moves to the super-tile wave that already holds that
+        // row-block's fragments: PAIR 20 -> 18, super waves 16 -> 17, every
+        // SIMD 34.  Wave 2 = (2I, 2I+2) takes tile 2I from its A side (PAIR
+        // wave 0, slab 0), 7 = (2I+1, 2I+3) tile 2I+1 (A, wave 0 slab 1),
+        // 6 = (2I+1, 2I+2) tile 2I+2 (B, wave 1 slab 0), 3 = (2I, 2I+3) tile
+        // 2I+3 (B, wave 1 slab 1).  Same MFMAs in the same order: bitwise equal.
+        const char *eb = getenv("BK_QUAD_BAL");
+        const bool full = w[0].kind == T_PAIR && w[1].kind == T_PAIR && st.size() == 4;
+        if (full && !(eb && atoi(eb) == 0)) {
+            w[0].xt = w[1].xt = 1;
+            w[0].cost = w[1].cost = COST_PAIR - 2;
+            const int xs[4][3] = {{2, 1, 0}, {7, 1, 1}, {6, 2, 2}, {3, 2, 3}};  // wave, side, slab
+            for (const auto &x : xs) {
+                w[x[0]].xt = x[1];
+                w[x[0]].xslot = x[2];
+                w[x[0]].cost = COST_OFF + 1;
+            }
+        }
         used[(size_t)I * TT + I + 1] = 1;
         groups.push_back(w);
     }
