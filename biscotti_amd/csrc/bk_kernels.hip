@@ -648,29 +648,31 @@ __device__ __forceinline__ void g3_dispatch(const T *__restrict__ X, int64_t ld,
                                             int nfull, int64_t d, const GroupDesc &G,
                                             const int *wd, char *lds, int wave, int lane,
                                             double *out, long long (&probe)[2]) {
-    const int xt = G.xt[wave];
+    // the balanced quads always stage 4 row-blocks: only NB = 4 (and the
+    // run-time NB = 0 of the ablation modes) carries the XT variants
+    const int xt = (NB == 4 || NB == 0) ? G.xt[wave] : 0;
     double *xout = out - (int64_t)wave * 2 * 4096 + (int64_t)G.xslot[wave] * 4096;
     switch (G.task[wave][0]) {
     case T_OFF:
         if (wave >= 4 && G3_STAGGER) {
             if (xt == 1)
-                g3_wave<T, T_OFF, MODE, true, NB, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+                g3_wave<T, T_OFF, MODE, true, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
             else if (xt == 2)
-                g3_wave<T, T_OFF, MODE, true, NB, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+                g3_wave<T, T_OFF, MODE, true, NB, (NB == 4 || NB == 0) ? 2 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
             else
                 g3_wave<T, T_OFF, MODE, true, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         } else {
             if (xt == 1)
-                g3_wave<T, T_OFF, MODE, false, NB, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+                g3_wave<T, T_OFF, MODE, false, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
             else if (xt == 2)
-                g3_wave<T, T_OFF, MODE, false, NB, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+                g3_wave<T, T_OFF, MODE, false, NB, (NB == 4 || NB == 0) ? 2 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
             else
                 g3_wave<T, T_OFF, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         }
         break;
     case T_PAIR:
         if (xt)
-            g3_wave<T, T_PAIR, MODE, false, NB, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+            g3_wave<T, T_PAIR, MODE, false, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         else
             g3_wave<T, T_PAIR, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
         break;
