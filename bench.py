@@ -244,6 +244,9 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-next-rows", action="store_true",
                     help="skip the §8(f) aggregation / quantised-sum / noise measurements")
+    ap.add_argument("--no-graph-probe", action="store_true",
+                    help="skip the eager-vs-hipGraph probe (keeps rocprof per-kernel averages "
+                         "to the headline shape)")
     ap.add_argument("--deterministic", action="store_true",
                     help="multi-GPU: all-gather + fixed-order sum instead of all-reduce")
     ap.add_argument("--sharded", action="store_true",
@@ -440,7 +443,7 @@ def main():
     if rank == 0 and world == 1 and not emu and not a.no_next_rows and w["dtype"] == "f64":
         out["next_rows"] = next_rows(eng, X, n, d, sel, m)
 
-    if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD:
+    if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD and not a.no_graph_probe:
         out["hip_graph"] = graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt)
 
     if rank == 0 and world == 1 and not emu and not a.no_e2e:
