@@ -110,7 +110,13 @@ __global__ __launch_bounds__(256) void k_noise(const double *delta, int64_t ld, 
                 d2v o;
                 o.x = a.x + s.x / dk;
                 o.y = a.y + s.y / dk;
+                // written once, not re-read by this kernel: a non-temporal store
+                // (0.839 -> 0.744 ms for 128 x 2^20 with k = 2, tools/ab_noise.py)
+#ifndef BK_NO_NT
+                __builtin_nontemporal_store(o, reinterpret_cast<d2v *>(out + i * old + c));
+#else
                 *reinterpret_cast<d2v *>(out + i * old + c) = o;
+#endif
             } else {
                 for (int64_t cc = c; cc < c + 2 && cc < d; ++cc) {
                     double s = 0.0;
