@@ -761,6 +761,44 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
                                                  const int *__restrict__ red,
                                                  const int *__restrict__ wglist,
                                                  double *__restrict__ U) {
+#ifndef BK_REDUCE_V1
+    // 64 elements per block, 2 per lane (16-B loads), 8 slabs in flight per
+    // sub-list; the same order of adds as below (bitwise the same U)
+    __shared__ d2v sub[8][32];
+    const int u = blockIdx.x >> 6, el = threadIdx.x & 31, q = threadIdx.x >> 5;
+    const int e = (blockIdx.x & 63) * 64 + el * 2;
+    const int off = red[3 * u], np = red[3 * u + 1], slot = red[3 * u + 2];
+    const int *wl = wglist + off;
+    d2v acc = {0.0, 0.0};
+    int s = q;
+    for (; s + 56 < np; s += 64) {
+        d2v v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            v[k] = *reinterpret_cast<const d2v *>(part + ((int64_t)wl[s + 8 * k] * 16 + slot) * 4096 + e);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            acc.x += v[k].x;
+            acc.y += v[k].y;
+        }
+    }
+    for (; s < np; s += 8) {
+        const d2v v = *reinterpret_cast<const d2v *>(part + ((int64_t)wl[s] * 16 + slot) * 4096 + e);
+        acc.x += v.x;
+        acc.y += v.y;
+    }
+    sub[q][el] = acc;
+    __syncthreads();
+    if (q == 0) {
+        d2v t = sub[0][el];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            t.x += sub[k][el].x;
+            t.y += sub[k][el].y;
+        }
+        *reinterpret_cast<d2v *>(U + (int64_t)u * 4096 + e) = t;
+    }
+#else
     __shared__ double sub[8][32];
     const int u = blockIdx.x >> 7, el = threadIdx.x & 31, q = threadIdx.x >> 5;
     const int e = (blockIdx.x & 127) * 32 + el;
@@ -787,6 +825,7 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
         for (int k = 1; k < 8; ++k) t += sub[k][el];
         U[(int64_t)u * 4096 + e] = t;
     }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1142,8 +1181,13 @@ hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, 
 }
 
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st) {
+#ifndef BK_REDUCE_V1
+    hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 64), dim3(256), 0, st, part, pl.d_red,
+                       pl.d_wglist, U);
+#else
     hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 128), dim3(256), 0, st, part, pl.d_red,
                        pl.d_wglist, U);
+#endif
     return hipGetLastError();
 }
 
