@@ -469,13 +469,34 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
     // offsets; a stage only adds the k-block's column.  Instruction i of a stage
     // moves rows 8ii..8ii+7 (128 B each) of slot b = i/8; lane L takes row
     // 8ii + L/8, granule (L&7) of the LDS row <- global granule (L&7)^(row&7).
-    const T *gsrc[G3_MAXB];
-    int gdst[G3_MAXB];
+    // ESPL: waves 0-3 issue NB + ESPL of the stage's 8 NB glds and waves 4-7
+    // NB - ESPL.  The timeline probe shows waves 0-3 waiting ~2,400-2,600
+    // cycles per k-block at the barrier and the staggered waves 4-7 ~100: the
+    // latter are the critical path, and each glds costs its wave ~100-185
+    // cycles of issue.  Super pairs 6 -> 8 / 4, quads 4 -> 6 / 2: K1 at D
+    // 4.07 -> 4.00 ms, the 8-GPU shard and C unchanged (profiles/r01/ab_gldssplit.log);
+    // -DBK_GLDS_E6=0 -DBK_GLDS_E4=0 restores the even split.
+#ifndef BK_GLDS_E6
+#define BK_GLDS_E6 2
+#endif
+#ifndef BK_GLDS_E4
+#define BK_GLDS_E4 2
+#endif
+    constexpr int ESPL = NB == 6 ? BK_GLDS_E6 : NB == 4 ? BK_GLDS_E4 : 0;
+    constexpr int CLO = NB + ESPL, CHI = NB - ESPL;
+    constexpr int GMAX = G3_MAXB + 2;
+    const bool hi = wave >= 4;
+    const T *gsrc[GMAX];
+    int gdst[GMAX];
     {
         const int rq = lane >> 3, j = lane & 7;
 #pragma unroll
-        for (int m = 0; m < G3_MAXB; ++m) {
-            const int i = wave + 8 * m;
+        for (int m = 0; m < GMAX; ++m) {
+            int i = wave + 8 * m;
+            if constexpr (ESPL != 0) {
+                i = hi ? 4 * CLO + (wave - 4) + 4 * m : wave + 4 * m;
+                if (i >= 8 * NB) i = 0;  // beyond this wave's count: never issued
+            }
             const int b = i >> 3, ii = i & 7;
             const int rl = ii * 8 + rq;
 #ifdef BK_K1_SAMEROWS  // timing-only ablation: every slot reads row-block 0 (all L2 hits)
@@ -490,10 +511,24 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
     auto issue = [&](int64_t kb, int stage) {
         const int64_t col = kb * BKE;
         char *base = lds + stage * G3_STAGE;
-#pragma unroll
 #ifndef BK_K1_GLDS_LIMIT  // timing-only ablation: issue at most this many glds per wave
 #define BK_K1_GLDS_LIMIT G3_MAXB
 #endif
+        if constexpr (ESPL != 0) {
+            if (hi) {
+#pragma unroll
+                for (int m = 0; m < CHI; ++m)
+                    __builtin_amdgcn_global_load_lds((const void *)(gsrc[m] + col),
+                                                     (void *)(base + gdst[m]), 16, 0, 0);
+            } else {
+#pragma unroll
+                for (int m = 0; m < CLO; ++m)
+                    __builtin_amdgcn_global_load_lds((const void *)(gsrc[m] + col),
+                                                     (void *)(base + gdst[m]), 16, 0, 0);
+            }
+            return;
+        }
+#pragma unroll
         for (int m = 0; m < (NB > 0 ? NB : G3_MAXB); ++m)
             if ((NB > 0 || m < c) && m < BK_K1_GLDS_LIMIT)
                 __builtin_amdgcn_global_load_lds((const void *)(gsrc[m] + col),
@@ -525,7 +560,16 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
     for (int t = 0; t < nk; ++t) {
         const int ahead = min(nk - t - 1, G3_STAGES - 2);  // stages issued after t
         G3_PROBE(p0);
-        if constexpr (NB > 0 && MODE != 2) {
+        if constexpr (NB > 0 && MODE != 2 && ESPL != 0) {
+            if (ahead > 0) {
+                if (hi)
+                    g3_waitc<CHI>();
+                else
+                    g3_waitc<CLO>();
+            } else {
+                g3_waitc<0>();
+            }
+        } else if constexpr (NB > 0 && MODE != 2) {
             if (ahead > 0)
                 g3_waitc<(NB < BK_K1_GLDS_LIMIT ? NB : BK_K1_GLDS_LIMIT)>();
             else
