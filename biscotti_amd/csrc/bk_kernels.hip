@@ -485,6 +485,7 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
     constexpr int ESPL = NB == 6 ? BK_GLDS_E6 : NB == 4 ? BK_GLDS_E4 : 0;
     constexpr int CLO = NB + ESPL, CHI = NB - ESPL;
     constexpr int GMAX = G3_MAXB + 2;
+    static_assert(CLO <= GMAX && CHI >= 0, "glds split exceeds the per-wave pointer table");
     const bool hi = wave >= 4;
     const T *gsrc[GMAX];
     int gdst[GMAX];
