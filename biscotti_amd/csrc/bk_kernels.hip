@@ -1067,6 +1067,53 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
     }
 }
 
+// fp32 rows with 16-B aligned starts: 4 columns per thread from one 16-B load
+// (the f2v form above moves 8 B per load: config E's K4 ran at 3.9 TB/s).  The
+// same per-column order of adds as k_mean, so the same bits.
+template <bool ACCUM>
+__global__ __launch_bounds__(256) void k_mean_f4(const float *__restrict__ X, int64_t ld, int64_t d,
+                                                 const int64_t *__restrict__ sel, int m,
+                                                 double *__restrict__ mean) {
+    extern __shared__ __attribute__((aligned(16))) int64_t srow[];
+    for (int r = threadIdx.x; r < m; r += 256) srow[r] = sel[r] * ld;
+    __syncthreads();
+    const double dm = (double)m;
+    const int64_t nq = (d + 3) >> 2;
+    for (int64_t cq = (int64_t)blockIdx.x * 256 + threadIdx.x; cq < nq;
+         cq += (int64_t)gridDim.x * 256) {
+        const int64_t c = cq * 4;
+        if (c + 3 < d) {
+            double acc[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[e] = ACCUM ? mean[c + e] : 0.0;
+            int r = 0;
+            for (; r + 8 <= m; r += 8) {
+                f4v v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    v[q] = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(X + srow[r + q] + c));
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[e] += (double)v[q][e];
+            }
+            for (; r < m; ++r) {
+                const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(X + srow[r] + c));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[e] += (double)v[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mean[c + e] = ACCUM ? acc[e] : acc[e] / dm;
+        } else {
+            for (int64_t cc = c; cc < d; ++cc) {
+                double acc = ACCUM ? mean[cc] : 0.0;
+                for (int r = 0; r < m; ++r) acc += (double)X[srow[r] + cc];
+                mean[cc] = ACCUM ? acc : acc / dm;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // synthetic batch: grid (column blocks, rows)
 // ---------------------------------------------------------------------------
@@ -1168,13 +1215,21 @@ static hipError_t launch_colsum(const void *X, int dtype, int64_t ld, int64_t d,
                                 int m, double *mean, int num_cu, hipStream_t st) {
     const int64_t npair = (d + 1) / 2;
     int64_t blocks = (npair + 255) / 256;
-    const int64_t cap = (int64_t)num_cu * 16;
+    const int64_t cap = (int64_t)num_cu * 16;  // 1, 2, 4, 8 per CU: no faster (v13 probe)
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     const size_t lds = (size_t)m * sizeof(int64_t);
     const bool vec = dtype == 0 ? ((ld % 2) == 0 && ((uintptr_t)X % 16) == 0)
                                 : ((ld % 2) == 0 && ((uintptr_t)X % 8) == 0);
     dim3 grid((unsigned)blocks), block(256);
+    if (dtype != 0 && (ld % 4) == 0 && ((uintptr_t)X % 16) == 0) {
+        int64_t b4 = ((d + 3) / 4 + 255) / 256;
+        if (b4 > (int64_t)num_cu * 16) b4 = (int64_t)num_cu * 16;
+        if (b4 < 1) b4 = 1;
+        hipLaunchKernelGGL((k_mean_f4<ACCUM>), dim3((unsigned)b4), block, lds, st, (const float *)X, ld,
+                           d, sel, m, mean);
+        return hipGetLastError();
+    }
     if (dtype == 0) {
         if (vec)
             hipLaunchKernelGGL((k_mean<double, true, ACCUM>), grid, block, lds, st, (const double *)X, ld, d,
@@ -1257,7 +1312,8 @@ hipError_t configure_kernels() {
                           (const void *)k_mean<double, true, true>,
                           (const void *)k_mean<double, false, true>,
                           (const void *)k_mean<float, true, true>,
-                          (const void *)k_mean<float, false, true>}) {
+                          (const void *)k_mean<float, false, true>,
+                          (const void *)k_mean_f4<false>, (const void *)k_mean_f4<true>}) {
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
         if (e != hipSuccess) return e;
     }
