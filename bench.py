@@ -232,6 +232,46 @@ def golden_check(name, sel_host, mean_local, c0, dl):
     return res
 
 
+def noised_probe(eng, dev, X, n, d, f, m, k=1):
+    """SURVEY §8(f) row 3 at the bench batch: bk_multikrum_noised from pinned
+    host Delta + k pinned noise vectors per update (noise added by K6 as the
+    rows land), against the same batch noised on the device
+    (bk_noise_apply_device + bk_multikrum_device): selection and mean bitwise."""
+    import ctypes
+    import torch
+    from biscotti_amd import _lib
+    g = torch.Generator(device=dev).manual_seed(7)
+    Nd = torch.randn((n, k, d), dtype=torch.float64, device=dev, generator=g) * 1e-4
+    Dh = torch.empty((n, d), dtype=torch.float64, pin_memory=True)
+    Dh.copy_(X[:, :d])
+    Nh = torch.empty((n, k, d), dtype=torch.float64, pin_memory=True)
+    Nh.copy_(Nd)
+    selh = np.empty(m, dtype=np.int64)
+    meanh = np.empty(d, dtype=np.float64)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        eng.multikrum_noised_ptr(Dh.data_ptr(), d, Nh.data_ptr(), k, d, _lib.BK_HOST_PINNED, n,
+                                 d, f, selh.ctypes.data, None, meanh.ctypes.data)
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    # reference on the device: noise a resident copy, then the device entry
+    Xn = torch.empty((n, d), dtype=torch.float64, device=dev)
+    eng.noise_apply_ptr(X.data_ptr(), n, d, X.stride(0), Nd.data_ptr(), k, d, Xn.data_ptr(), d)
+    sel2 = torch.empty(m, dtype=torch.int64, device=dev)
+    mean2 = torch.empty(d, dtype=torch.float64, device=dev)
+    eng.multikrum_device_ptr(Xn.data_ptr(), _lib.BK_F64, n, d, d, f, sel2.data_ptr(), None,
+                             mean2.data_ptr())
+    torch.cuda.synchronize()
+    same_sel = bool(np.array_equal(selh, sel2.cpu().numpy()))
+    same_mean = bool(np.array_equal(meanh.view(np.int64), mean2.cpu().numpy().view(np.int64)))
+    del Xn, Nd, Dh, Nh
+    return {"k": k, "ms": round(t * 1e3, 3),
+            "GB_per_s": round(n * d * 8 / t / 1e9, 3),
+            "pcie_GB_per_s": round(n * d * 8 * (1 + k) / t / 1e9, 3),
+            "selected_set_same": same_sel, "mean_bitwise_same": same_mean}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -471,6 +511,9 @@ def main():
                                      "selected_set_same": bool(np.array_equal(
                                          selh, sel.cpu().numpy()))}
         del Xh
+
+    if rank == 0 and world == 1 and not emu and not a.no_e2e and w["dtype"] == "f64":
+        out["e2e_noised_pinned"] = noised_probe(eng, dev, X, n, dl, f, m)
 
     if rank == 0 and world == 1 and not emu and not a.no_cpu_baseline:
         try:

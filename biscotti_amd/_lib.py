@@ -16,7 +16,7 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
-BK_ABI_VERSION = 4
+BK_ABI_VERSION = 5
 KERNELS = ["k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni"]
 K = {name: i for i, name in enumerate(KERNELS)}
@@ -61,6 +61,8 @@ SIGNATURES = {
     "bk_aggregate": (_i, [_p, _p, _i, _i, _i64, _i64, _i64, _p, _i64, _p]),
     "bk_quantized_sum_device": (_i, [_p, _p, _i, _i64, _i64, _i64, _p, _i64, _i, _p, _p]),
     "bk_noise_apply_device": (_i, [_p, _p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64]),
+    "bk_multikrum_noised": (_i, [_p, _p, _i64, _p, _i64, _i64, _i, _i64, _i64, _i64, _p, _p,
+                                 _p, _p, _p, _i64]),
     "bk_roni_device": (_i, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _i64, _i64, _p]),
     "bk_roni_set_validation": (_i, [_p, _p, _i64, _i64, _i64, _p]),
     "bk_roni": (_i, [_p, _p, _p, _i64, _i64, _i64, _p]),

@@ -81,6 +81,11 @@ struct bk_ctx {
     // RONI: the validation set (bk_roni_set_validation) and per-call scratch
     DevBuf roni_X, roni_y, roni_w, roni_d, roni_cnt, roni_s;
     int64_t roni_nv = 0, roni_dim = 0;
+    // bk_multikrum_noised: a 2-slot ring of noise chunks, filled on a copy
+    // stream while K6 consumes the previous chunk on `stream` (created lazily)
+    DevBuf noise;
+    hipStream_t copy = nullptr;
+    hipEvent_t ev_go = nullptr, ev_cp[2] = {nullptr, nullptr}, ev_use[2] = {nullptr, nullptr};
     // host-side pinned allocations handed out by bk_stage_alloc
     std::vector<void *> staged;
     // timing
@@ -157,7 +162,8 @@ void drop_graph(bk_ctx::CachedGraph &cg) {
 void bind_epoch(bk_ctx *c) {
     DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,   &c->scores, &c->mask,   &c->sel,
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
-                      &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s};
+                      &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
+                      &c->noise};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -384,6 +390,35 @@ int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
     return stage_finish(c, U, pl, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
 }
 
+// K1..K4 on a device-resident batch staged by a host entry, then the outputs
+// back to the caller's host arrays (bk_multikrum, bk_multikrum_noised)
+int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t dld,
+                     int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
+                     double *mean_out) {
+    const int64_t m = n - f;
+    CHK(ensure(c->sel, (size_t)n * sizeof(int64_t)));
+    CHK(ensure(c->scores, (size_t)n * sizeof(double)));
+    if (mean_out) CHK(ensure(c->mean, (size_t)d * sizeof(double)));
+    int64_t *dsel = (int64_t *)c->sel.p;
+    double *dsc = (double *)c->scores.p;
+    double *dmean = mean_out ? (double *)c->mean.p : nullptr;
+    CHK(run_device(c, dX, dtype, n, d, dld, f, dsel, dsc, dmean));
+    CHK(timed(c, BK_K_D2H, [&] {
+        hipError_t e = hipMemcpyAsync(sel_idx, dsel, (size_t)m * sizeof(int64_t),
+                                      hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess && scores)
+            e = hipMemcpyAsync(scores, dsc, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream);
+        if (e == hipSuccess && mean_out)
+            e = hipMemcpyAsync(mean_out, dmean, (size_t)d * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream);
+        return e;
+    }));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (m_out) *m_out = m;
+    return BK_OK;
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -465,9 +500,14 @@ void bk_destroy(bk_ctx *c) {
         (void)hipStreamSynchronize(c->stream);
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->scores,
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
-                          &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s};
+                          &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
+                          &c->noise};
+        if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
+        for (hipEvent_t ev : {c->ev_go, c->ev_cp[0], c->ev_cp[1], c->ev_use[0], c->ev_use[1]})
+            if (ev) (void)hipEventDestroy(ev);
+        if (c->copy) (void)hipStreamDestroy(c->copy);
         for (void *p : c->staged) (void)hipHostFree(p);
         for (auto &ev : c->pending) {
             (void)hipEventDestroy(ev.a);
@@ -646,28 +686,78 @@ int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
         }));
         dX = dst;
     }
-    const int64_t m = n - f;
-    CHK(ensure(c->sel, (size_t)n * sizeof(int64_t)));
-    CHK(ensure(c->scores, (size_t)n * sizeof(double)));
-    if (mean_out) CHK(ensure(c->mean, (size_t)d * sizeof(double)));
-    int64_t *dsel = (int64_t *)c->sel.p;
-    double *dsc = (double *)c->scores.p;
-    double *dmean = mean_out ? (double *)c->mean.p : nullptr;
-    CHK(run_device(c, dX, dtype, n, d, dld, f, dsel, dsc, dmean));
-    CHK(timed(c, BK_K_D2H, [&] {
-        hipError_t e = hipMemcpyAsync(sel_idx, dsel, (size_t)m * sizeof(int64_t),
-                                      hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess && scores)
-            e = hipMemcpyAsync(scores, dsc, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
-                               c->stream);
-        if (e == hipSuccess && mean_out)
-            e = hipMemcpyAsync(mean_out, dmean, (size_t)d * sizeof(double), hipMemcpyDeviceToHost,
-                               c->stream);
-        return e;
-    }));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (m_out) *m_out = m;
-    return BK_OK;
+    return run_host_outputs(c, dX, dtype, n, d, dld, f, sel_idx, m_out, scores, mean_out);
+}
+
+// the noise application fused into the H2D staging of
+// the verifier batch.  Rows go over in chunks on a copy stream (Delta rows
+// straight into the padded device batch, their k noise vectors into a 2-slot
+// ring); K6 adds each chunk's noise in place on the compute stream while the
+// next chunk is in flight.  No host pass over n*d, and no n*k*d device buffer.
+int bk_multikrum_noised(bk_ctx *c, const double *delta, int64_t ld, const double *noise,
+                        int64_t k, int64_t noise_ld, int where, int64_t n, int64_t d, int64_t f,
+                        int64_t *sel_idx, int64_t *m_out, double *scores, double *mean_out,
+                        double *noised_out, int64_t out_ld) {
+    CHK(check_common(c, delta, BK_F64, n, d, ld));
+    CHK(bk_check_args(n, d, f));
+    if (!sel_idx) return fail(BK_EINVAL, "null sel_idx");
+    if (where != BK_HOST && where != BK_HOST_PINNED)
+        return fail(BK_EINVAL, "bad where=%d (host batches only; device-resident batches use "
+                               "bk_noise_apply_device + bk_multikrum_device)", where);
+    if (k < 0) return fail(BK_EINVAL, "k=%lld < 0", (long long)k);
+    if (k > 0 && !noise) return fail(BK_EINVAL, "null noise with k=%lld", (long long)k);
+    if (k > 0 && noise_ld < d) return fail(BK_EINVAL, "noise_ld=%lld < d", (long long)noise_ld);
+    if (noised_out && out_ld < d) return fail(BK_EINVAL, "out_ld=%lld < d", (long long)out_ld);
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    if (!c->copy) {
+        HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+        for (hipEvent_t *ev : {&c->ev_go, &c->ev_cp[0], &c->ev_cp[1], &c->ev_use[0], &c->ev_use[1]})
+            HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    }
+    const int64_t dld = (d + 1) / 2 * 2;  // 16-B rows: K1 v3 applies
+    CHK(ensure(c->X, (size_t)n * dld * sizeof(double)));
+    double *dX = (double *)c->X.p;
+    // chunk: rows whose noise fills <= BK_NOISE_CHUNK_BYTES (default 64 MiB) per ring slot
+    int64_t cap = (int64_t)64 << 20;
+    if (const char *v = getenv("BK_NOISE_CHUNK_BYTES")) cap = atoll(v) > 0 ? atoll(v) : cap;
+    const int64_t row_noise = k * d * (int64_t)sizeof(double);
+    int64_t R = row_noise > 0 ? cap / row_noise : n;
+    R = R < 1 ? 1 : R > n ? n : R;
+    double *ring = nullptr;
+    if (k > 0) {
+        CHK(ensure(c->noise, (size_t)2 * R * k * d * sizeof(double)));
+        ring = (double *)c->noise.p;
+    }
+    // earlier work on the compute stream may still read the batch / the ring
+    HIPCHK(hipEventRecord(c->ev_go, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->copy, c->ev_go, 0));
+    for (int64_t i0 = 0, ch = 0; i0 < n; i0 += R, ++ch) {
+        const int64_t rows = n - i0 < R ? n - i0 : R;
+        const int s = (int)(ch & 1);
+        double *slot = ring ? ring + (size_t)s * R * k * d : nullptr;
+        if (ch >= 2 && k > 0) HIPCHK(hipStreamWaitEvent(c->copy, c->ev_use[s], 0));
+        HIPCHK(hipMemcpy2DAsync(dX + i0 * dld, (size_t)dld * 8, delta + i0 * ld, (size_t)ld * 8,
+                                (size_t)d * 8, (size_t)rows, hipMemcpyHostToDevice, c->copy));
+        if (k > 0)
+            HIPCHK(hipMemcpy2DAsync(slot, (size_t)d * 8, noise + i0 * k * noise_ld,
+                                    (size_t)noise_ld * 8, (size_t)d * 8, (size_t)(rows * k),
+                                    hipMemcpyHostToDevice, c->copy));
+        HIPCHK(hipEventRecord(c->ev_cp[s], c->copy));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_cp[s], 0));
+        // k = 0: no noisers, NoisedDelta = Delta (main.go:1599-1602)
+        if (k > 0) {
+            CHK(timed(c, BK_K_NOISE, [&] {
+                return launch_noise(dX + i0 * dld, dld, rows, d, slot, k, d, dX + i0 * dld, dld,
+                                    c->num_cu, c->stream);
+            }));
+            HIPCHK(hipEventRecord(c->ev_use[s], c->stream));
+        }
+    }
+    if (noised_out)
+        HIPCHK(hipMemcpy2DAsync(noised_out, (size_t)out_ld * 8, dX, (size_t)dld * 8,
+                                (size_t)d * 8, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    return run_host_outputs(c, dX, BK_F64, n, d, dld, f, sel_idx, m_out, scores, mean_out);
 }
 
 int bk_gram_upper_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,

@@ -152,6 +152,52 @@ class Engine:
         assert mo.value == m
         return sel, sc, mean
 
+    # ---- host entry with the noise applied in the H2D staging -----------
+    #      (bk_multikrum_noised) -------------------
+    def multikrum_noised(self, delta, noise, f, want_scores=True, want_mean=True,
+                         want_noised=False):
+        """Multi-Krum of NoisedDelta = delta + mean of the k noise vectors
+        (main.go:1524-1537, 1606-1653) with the noise added on the device as
+        the rows land.  delta (n, d) fp64; noise (n, k, d) fp64, k >= 0 (k = 0:
+        no noisers, NoisedDelta = Delta).  Returns (sel, scores, mean, noised)."""
+        D = np.asarray(delta, dtype=np.float64)
+        if D.ndim != 2:
+            raise ValueError("delta must be 2-D (n updates x d)")
+        if D.strides[1] != 8 or D.strides[0] % 8:
+            D = np.ascontiguousarray(D)
+        n, d = D.shape
+        N = np.ascontiguousarray(noise, dtype=np.float64)
+        if N.ndim != 3 or N.shape[0] != n or (N.shape[1] > 0 and N.shape[2] != d):
+            raise ValueError("noise must be (n, k, d) matching delta (n, d)")
+        k = N.shape[1]
+        f = int(f)
+        check(lib().bk_check_args(n, d, f))
+        m = n - f
+        sel = np.empty(m, dtype=np.int64)
+        mo = ctypes.c_int64(0)
+        sc = np.empty(n, dtype=np.float64) if want_scores else None
+        mean = np.empty(d, dtype=np.float64) if want_mean else None
+        out = np.empty((n, d), dtype=np.float64) if want_noised else None
+        check(lib().bk_multikrum_noised(self._ctx, D.ctypes.data, D.strides[0] // 8,
+                                        N.ctypes.data if k else None, k, d, _lib.BK_HOST, n, d,
+                                        f, sel.ctypes.data, ctypes.addressof(mo),
+                                        sc.ctypes.data if sc is not None else None,
+                                        mean.ctypes.data if mean is not None else None,
+                                        out.ctypes.data if out is not None else None, d))
+        assert mo.value == m
+        return sel, sc, mean, out
+
+    def multikrum_noised_ptr(self, delta_ptr, ld, noise_ptr, k, noise_ld, where, n, d, f,
+                             sel_ptr, scores_ptr=None, mean_ptr=None, noised_ptr=None,
+                             out_ld=0):
+        """Raw host pointers (e.g. pinned torch tensors); outputs are host pointers."""
+        mo = ctypes.c_int64(0)
+        check(lib().bk_multikrum_noised(self._ctx, _p(delta_ptr), ld, _p(noise_ptr), k, noise_ld,
+                                        where, n, d, f, _p(sel_ptr), ctypes.addressof(mo),
+                                        _p(scores_ptr), _p(mean_ptr), _p(noised_ptr),
+                                        out_ld or d))
+        return mo.value
+
     # ---- device entry (bk_multikrum_device): raw device pointers --------
     def multikrum_device_ptr(self, x_ptr, dtype, n, d, ld, f, sel_ptr, scores_ptr=None,
                              mean_ptr=None):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 4
+#define BK_ABI_VERSION 5
 
 typedef struct bk_ctx bk_ctx;
 
@@ -202,6 +202,25 @@ int bk_quantized_sum_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, i
 int bk_noise_apply_device(bk_ctx *ctx, const double *d_delta, int64_t n, int64_t d, int64_t ld,
                           const double *d_noise, int64_t k, int64_t noise_ld, double *d_out,
                           int64_t out_ld);
+
+/* Noise application fused into the verifier's H2D staging (SURVEY.md §8(f)
+ * row 3), then the drop-in Multi-Krum of bk_multikrum on the noised batch.
+ * Replaces the host pass NoisedDelta = Delta + noise (main.go:1524-1537,
+ * 1606-1653) that precedes getTopKRUMIndex (krum.go:100-166) when the batch is
+ * noised where it is verified.  delta: host n x d (row stride ld); noise: host,
+ * vector j of update i at noise + (i*k + j) * noise_ld.  Rows cross PCIe in
+ * chunks on a copy stream while K6 noises the previous chunk in place on the
+ * context stream (BK_NOISE_CHUNK_BYTES, default 64 MiB of noise per chunk).
+ * k = 0 means no noisers: NoisedDelta = Delta (main.go:1599-1602; unlike
+ * bk_noise_apply_device, whose k = 0 is the literal 0/0).  where is BK_HOST or
+ * BK_HOST_PINNED (pinned memory overlaps; pageable copies are staged by HIP).
+ * Outputs as bk_multikrum, plus noised_out (nullable, host n x d, row stride
+ * out_ld): the noised batch, bit-identical to bk_noise_apply_device.
+ * Synchronous. */
+int bk_multikrum_noised(bk_ctx *ctx, const double *delta, int64_t ld, const double *noise,
+                        int64_t k, int64_t noise_ld, int where, int64_t n, int64_t d, int64_t f,
+                        int64_t *sel_idx, int64_t *m_out, double *scores, double *mean_out,
+                        double *noised_out, int64_t out_ld);
 
 /* RONI verifier -- roni(ww, delta),
  * ML/code/logistic_validator.py:22-33, batched over n updates:
