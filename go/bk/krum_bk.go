@@ -128,3 +128,81 @@ func (krumval *KRUMValidator) getTopKRUMIndex(deltas [][]float64) []int {
 	}
 	return out
 }
+
+// getTopKRUMIndexNoised is the same verifier call for updates that carry Delta
+// and the averaged Noise vector separately (update.go:13-22; NoisedDelta =
+// Delta + Noise at main.go:1524-1537): the noise is added on the GPU while the
+// batch crosses PCIe (bk_multikrum_noised, SURVEY.md §8(f) row 3), so the
+// verifier never builds NoisedDelta on the host.  k = 1 (Noise is already the
+// mean over the noisers, main.go:1606-1653), which is bitwise Delta[i] +
+// Noise[i]; updates without noise (-np=false) go with k = 0.  A batch that
+// mixes the two falls back to getTopKRUMIndex over NoisedDelta.
+func (krumval *KRUMValidator) getTopKRUMIndexNoised(updates []Update) []int {
+	n := len(updates)
+	if n == 0 || bkCtx == nil || bkGroup != nil {
+		return krumval.getTopKRUMIndex(noisedDeltas(updates))
+	}
+	d := len(updates[0].Delta)
+	k := 0
+	if len(updates[0].Noise) > 0 {
+		k = 1
+	}
+	for i := range updates {
+		if len(updates[i].Delta) != d || len(updates[i].Noise) != k*d {
+			return krumval.getTopKRUMIndex(noisedDeltas(updates))
+		}
+	}
+	f := int(krumval.NumAdversaries * float64(n))
+	if C.bk_check_args(C.int64_t(n), C.int64_t(d), C.int64_t(f)) != C.BK_OK {
+		outLog.Printf("Krum: %s", C.GoString(C.bk_last_error()))
+		return []int{}
+	}
+	need := int64(n) * int64(d) * 8 * int64(1+k)
+	if need > bkStageLen {
+		if bkStage != nil {
+			C.bk_stage_free(bkCtx, bkStage)
+		}
+		var p unsafe.Pointer
+		if C.bk_stage_alloc(bkCtx, C.int64_t(need), &p) != C.BK_OK {
+			outLog.Printf("Krum: %s", C.GoString(C.bk_last_error()))
+			bkStage, bkStageLen = nil, 0
+			return []int{}
+		}
+		bkStage, bkStageLen = p, need
+	}
+	// pinned staging: Delta rows, then (k = 1) the Noise rows
+	stage := unsafe.Slice((*float64)(bkStage), n*d*(1+k))
+	for i := 0; i < n; i++ {
+		copy(stage[i*d:(i+1)*d], updates[i].Delta)
+		if k == 1 {
+			copy(stage[(n+i)*d:(n+i+1)*d], updates[i].Noise)
+		}
+	}
+	var noise *C.double
+	if k == 1 {
+		noise = (*C.double)(unsafe.Pointer(&stage[n*d]))
+	}
+	m := n - f
+	sel := make([]C.int64_t, m)
+	var mOut C.int64_t
+	st := C.bk_multikrum_noised(bkCtx, (*C.double)(bkStage), C.int64_t(d), noise, C.int64_t(k),
+		C.int64_t(d), C.BK_HOST_PINNED, C.int64_t(n), C.int64_t(d), C.int64_t(f),
+		(*C.int64_t)(unsafe.Pointer(&sel[0])), &mOut, nil, nil, nil, 0)
+	if st != C.BK_OK {
+		outLog.Printf("Krum failed (%d): %s", int(st), C.GoString(C.bk_last_error()))
+		return []int{}
+	}
+	out := make([]int, int(mOut))
+	for i := range out {
+		out[i] = int(sel[i])
+	}
+	return out
+}
+
+func noisedDeltas(updates []Update) [][]float64 {
+	deltas := make([][]float64, len(updates))
+	for i := range updates {
+		deltas[i] = updates[i].NoisedDelta
+	}
+	return deltas
+}
