@@ -390,11 +390,81 @@ int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
     return stage_finish(c, U, pl, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
 }
 
-// K1..K4 on a device-resident batch staged by a host entry, then the outputs
-// back to the caller's host arrays (bk_multikrum, bk_multikrum_noised)
+// Host entries (bk_multikrum, bk_multikrum_noised): the batch crosses PCIe in
+// column chunks on a copy stream, and each chunk's partial Gram (K1 + K1b,
+// after K6 when noise is applied) runs on the compute stream while the next
+// chunk is in flight.  The Gram is additive over columns, so only the last
+// chunk's K1 and the finish remain after the copies; the chunk partials are
+// summed in chunk order (deterministic).  Noise: vector j of update i at
+// noise + (i*k + j) * noise_ld, staged per chunk in a 2-slot device ring.
+// On return (async) the device batch dX (row stride dld) is complete and
+// noised and U holds the full packed Gram; pl describes it for stage_finish.
+int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const double *noise,
+                         int64_t k, int64_t noise_ld, int64_t n, int64_t d, char *dX,
+                         int64_t dld, double *U, Plan &pl) {
+    const size_t es = esize(dtype);
+    if (!c->copy) {
+        HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+        for (hipEvent_t *ev : {&c->ev_go, &c->ev_cp[0], &c->ev_cp[1], &c->ev_use[0], &c->ev_use[1]})
+            HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    }
+    // chunks of ~BK_STAGE_CHUNK_BYTES (default 256 MiB) of the batch plus its
+    // noise; widths a multiple of 64 columns (16-B aligned chunk starts)
+    int64_t cap = (int64_t)256 << 20;
+    if (const char *v = getenv("BK_STAGE_CHUNK_BYTES")) cap = atoll(v) > 0 ? atoll(v) : cap;
+    const int64_t col_bytes = n * (int64_t)es + n * k * (int64_t)sizeof(double);
+    int64_t W = cap / col_bytes;
+    W = W < 64 ? 64 : W / 64 * 64;
+    if (W >= d) W = d;
+    const int64_t C = (d + W - 1) / W;
+    if (C > 1024) return fail(BK_EINVAL, "BK_STAGE_CHUNK_BYTES too small (%lld chunks)", (long long)C);
+    const size_t usz = (size_t)bk_upper_elems(n);
+    double *Ug = U;
+    if (C > 1) {
+        CHK(ensure(c->Ug, usz * C * sizeof(double)));
+        Ug = (double *)c->Ug.p;
+    }
+    double *ring = nullptr;
+    if (k > 0) {
+        CHK(ensure(c->noise, (size_t)2 * n * k * W * sizeof(double)));
+        ring = (double *)c->noise.p;
+    }
+    // earlier work on the compute stream may still read the batch / the ring
+    HIPCHK(hipEventRecord(c->ev_go, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->copy, c->ev_go, 0));
+    for (int64_t ch = 0; ch < C; ++ch) {
+        const int64_t c0 = ch * W, wc = d - c0 < W ? d - c0 : W;
+        const int s = (int)(ch & 1);
+        double *slot = ring ? ring + (size_t)s * n * k * W : nullptr;
+        if (ch >= 2 && k > 0) HIPCHK(hipStreamWaitEvent(c->copy, c->ev_use[s], 0));
+        HIPCHK(hipMemcpy2DAsync(dX + c0 * es, (size_t)dld * es, (const char *)X + c0 * es,
+                                (size_t)ld * es, (size_t)wc * es, (size_t)n,
+                                hipMemcpyHostToDevice, c->copy));
+        if (k > 0)
+            HIPCHK(hipMemcpy2DAsync(slot, (size_t)wc * 8, noise + c0, (size_t)noise_ld * 8,
+                                    (size_t)wc * 8, (size_t)(n * k), hipMemcpyHostToDevice,
+                                    c->copy));
+        HIPCHK(hipEventRecord(c->ev_cp[s], c->copy));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_cp[s], 0));
+        double *xc = (double *)(dX + c0 * es);
+        if (k > 0) {
+            CHK(timed(c, BK_K_NOISE, [&] {
+                return launch_noise(xc, dld, n, wc, slot, k, wc, xc, dld, c->num_cu, c->stream);
+            }));
+            HIPCHK(hipEventRecord(c->ev_use[s], c->stream));
+        }
+        CHK(stage_gram(c, dX + c0 * es, dtype, n, wc, dld, Ug + (size_t)ch * usz, pl));
+    }
+    if (C > 1) HIPCHK(launch_sum_ranks(Ug, (int)C, (int64_t)usz, U, c->stream));
+    pl.d = d;
+    return BK_OK;
+}
+
+// K2..K4 on a batch staged by stage_host_pipelined, then the outputs back to
+// the caller's host arrays (bk_multikrum, bk_multikrum_noised)
 int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t dld,
-                     int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
-                     double *mean_out) {
+                     int64_t f, const double *U, const Plan &pl, int64_t *sel_idx,
+                     int64_t *m_out, double *scores, double *mean_out) {
     const int64_t m = n - f;
     CHK(ensure(c->sel, (size_t)n * sizeof(int64_t)));
     CHK(ensure(c->scores, (size_t)n * sizeof(double)));
@@ -402,7 +472,7 @@ int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
     int64_t *dsel = (int64_t *)c->sel.p;
     double *dsc = (double *)c->scores.p;
     double *dmean = mean_out ? (double *)c->mean.p : nullptr;
-    CHK(run_device(c, dX, dtype, n, d, dld, f, dsel, dsc, dmean));
+    CHK(stage_finish(c, U, pl, dX, dtype, n, d, dld, f, dsel, dsc, dmean));
     CHK(timed(c, BK_K_D2H, [&] {
         hipError_t e = hipMemcpyAsync(sel_idx, dsel, (size_t)m * sizeof(int64_t),
                                       hipMemcpyDeviceToHost, c->stream);
@@ -672,21 +742,21 @@ int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
     const size_t es = esize(dtype);
     const void *dX = X;
     int64_t dld = ld;
+    CHK(ensure(c->U, (size_t)bk_upper_elems(n) * sizeof(double)));
+    double *U = (double *)c->U.p;
+    Plan pl;
     if (where != BK_DEVICE) {
         // device rows padded to 16 B so K1 v3 (global_load_lds granules) always applies
         const int64_t epg = (int64_t)(16 / es);
         dld = (d + epg - 1) / epg * epg;
         CHK(ensure(c->X, (size_t)n * dld * es));
-        void *dst = c->X.p;
-        CHK(timed(c, BK_K_H2D, [&] {
-            if (ld == d && dld == d)
-                return hipMemcpyAsync(dst, X, (size_t)n * d * es, hipMemcpyHostToDevice, c->stream);
-            return hipMemcpy2DAsync(dst, (size_t)dld * es, X, (size_t)ld * es, (size_t)d * es,
-                                    (size_t)n, hipMemcpyHostToDevice, c->stream);
-        }));
-        dX = dst;
+        CHK(stage_host_pipelined(c, X, ld, dtype, nullptr, 0, 0, n, d, (char *)c->X.p, dld, U,
+                                 pl));
+        dX = c->X.p;
+    } else {
+        CHK(stage_gram(c, dX, dtype, n, d, dld, U, pl));
     }
-    return run_host_outputs(c, dX, dtype, n, d, dld, f, sel_idx, m_out, scores, mean_out);
+    return run_host_outputs(c, dX, dtype, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out);
 }
 
 // the noise application fused into the H2D staging of
@@ -710,54 +780,19 @@ int bk_multikrum_noised(bk_ctx *c, const double *delta, int64_t ld, const double
     if (noised_out && out_ld < d) return fail(BK_EINVAL, "out_ld=%lld < d", (long long)out_ld);
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
-    if (!c->copy) {
-        HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
-        for (hipEvent_t *ev : {&c->ev_go, &c->ev_cp[0], &c->ev_cp[1], &c->ev_use[0], &c->ev_use[1]})
-            HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-    }
     const int64_t dld = (d + 1) / 2 * 2;  // 16-B rows: K1 v3 applies
     CHK(ensure(c->X, (size_t)n * dld * sizeof(double)));
     double *dX = (double *)c->X.p;
-    // chunk: rows whose noise fills <= BK_NOISE_CHUNK_BYTES (default 64 MiB) per ring slot
-    int64_t cap = (int64_t)64 << 20;
-    if (const char *v = getenv("BK_NOISE_CHUNK_BYTES")) cap = atoll(v) > 0 ? atoll(v) : cap;
-    const int64_t row_noise = k * d * (int64_t)sizeof(double);
-    int64_t R = row_noise > 0 ? cap / row_noise : n;
-    R = R < 1 ? 1 : R > n ? n : R;
-    double *ring = nullptr;
-    if (k > 0) {
-        CHK(ensure(c->noise, (size_t)2 * R * k * d * sizeof(double)));
-        ring = (double *)c->noise.p;
-    }
-    // earlier work on the compute stream may still read the batch / the ring
-    HIPCHK(hipEventRecord(c->ev_go, c->stream));
-    HIPCHK(hipStreamWaitEvent(c->copy, c->ev_go, 0));
-    for (int64_t i0 = 0, ch = 0; i0 < n; i0 += R, ++ch) {
-        const int64_t rows = n - i0 < R ? n - i0 : R;
-        const int s = (int)(ch & 1);
-        double *slot = ring ? ring + (size_t)s * R * k * d : nullptr;
-        if (ch >= 2 && k > 0) HIPCHK(hipStreamWaitEvent(c->copy, c->ev_use[s], 0));
-        HIPCHK(hipMemcpy2DAsync(dX + i0 * dld, (size_t)dld * 8, delta + i0 * ld, (size_t)ld * 8,
-                                (size_t)d * 8, (size_t)rows, hipMemcpyHostToDevice, c->copy));
-        if (k > 0)
-            HIPCHK(hipMemcpy2DAsync(slot, (size_t)d * 8, noise + i0 * k * noise_ld,
-                                    (size_t)noise_ld * 8, (size_t)d * 8, (size_t)(rows * k),
-                                    hipMemcpyHostToDevice, c->copy));
-        HIPCHK(hipEventRecord(c->ev_cp[s], c->copy));
-        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_cp[s], 0));
-        // k = 0: no noisers, NoisedDelta = Delta (main.go:1599-1602)
-        if (k > 0) {
-            CHK(timed(c, BK_K_NOISE, [&] {
-                return launch_noise(dX + i0 * dld, dld, rows, d, slot, k, d, dX + i0 * dld, dld,
-                                    c->num_cu, c->stream);
-            }));
-            HIPCHK(hipEventRecord(c->ev_use[s], c->stream));
-        }
-    }
+    CHK(ensure(c->U, (size_t)bk_upper_elems(n) * sizeof(double)));
+    double *U = (double *)c->U.p;
+    Plan pl;
+    // k = 0: no noisers, NoisedDelta = Delta (main.go:1599-1602)
+    CHK(stage_host_pipelined(c, delta, ld, BK_F64, k > 0 ? noise : nullptr, k, noise_ld, n, d,
+                             (char *)dX, dld, U, pl));
     if (noised_out)
         HIPCHK(hipMemcpy2DAsync(noised_out, (size_t)out_ld * 8, dX, (size_t)dld * 8,
                                 (size_t)d * 8, (size_t)n, hipMemcpyDeviceToHost, c->stream));
-    return run_host_outputs(c, dX, BK_F64, n, d, dld, f, sel_idx, m_out, scores, mean_out);
+    return run_host_outputs(c, dX, BK_F64, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out);
 }
 
 int bk_gram_upper_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,

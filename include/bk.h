@@ -82,6 +82,9 @@ int bk_stage_free(bk_ctx *ctx, void *pinned);
 
 /* ---- the drop-in: getTopKRUMIndex (krum.go:100-166) + numpy krum ---------
  * X on host (BK_HOST / BK_HOST_PINNED: copied H2D) or device (BK_DEVICE).
+ * A host batch crosses PCIe in column chunks (BK_STAGE_CHUNK_BYTES, default
+ * 256 MiB) on a copy stream while the previous chunk's partial Gram runs; the
+ * chunk partials are summed in chunk order, so results are deterministic.
  * Outputs are HOST pointers: sel_idx (m entries), m_out, scores (n, nullable),
  * mean_out (d, nullable).  Synchronous. */
 int bk_multikrum(bk_ctx *ctx, const void *X, int where, int dtype, int64_t n, int64_t d,
@@ -208,9 +211,9 @@ int bk_noise_apply_device(bk_ctx *ctx, const double *d_delta, int64_t n, int64_t
  * Replaces the host pass NoisedDelta = Delta + noise (main.go:1524-1537,
  * 1606-1653) that precedes getTopKRUMIndex (krum.go:100-166) when the batch is
  * noised where it is verified.  delta: host n x d (row stride ld); noise: host,
- * vector j of update i at noise + (i*k + j) * noise_ld.  Rows cross PCIe in
- * chunks on a copy stream while K6 noises the previous chunk in place on the
- * context stream (BK_NOISE_CHUNK_BYTES, default 64 MiB of noise per chunk).
+ * vector j of update i at noise + (i*k + j) * noise_ld.  Column chunks cross
+ * PCIe on a copy stream while K6 noises, and K1 takes the partial Gram of, the
+ * previous chunk on the context stream (as bk_multikrum's host path).
  * k = 0 means no noisers: NoisedDelta = Delta (main.go:1599-1602; unlike
  * bk_noise_apply_device, whose k = 0 is the literal 0/0).  where is BK_HOST or
  * BK_HOST_PINNED (pinned memory overlaps; pageable copies are staged by HIP).
