@@ -1036,7 +1036,9 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
     const int64_t m = n - f;
     const int64_t usz = bk_upper_elems(n);
     std::vector<Plan> pls((size_t)G);
-    // 1. per device: H2D of its column shard, partial Gram (K1 + K1b)
+    // 1. per device: its column shard crosses PCIe in column chunks on the
+    //    device's copy stream, each chunk's partial Gram (K1 + K1b) overlapped
+    //    with the next chunk's copy (stage_host_pipelined)
     for (int r = 0; r < G; ++r) {
         bk_ctx *c = g->ctx[(size_t)r];
         DeviceGuard dg(c->device);
@@ -1044,13 +1046,9 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
         group_shard(d, G, r, &c0, &dl);
         CHK(ensure(g->X[(size_t)r], (size_t)n * dl * es));
         CHK(ensure(g->U[(size_t)r], (size_t)usz * sizeof(double)));
-        void *dst = g->X[(size_t)r].p;
         const char *src = (const char *)X + (size_t)c0 * es;
-        CHK(timed(c, BK_K_H2D, [&] {
-            return hipMemcpy2DAsync(dst, (size_t)dl * es, src, (size_t)ld * es, (size_t)dl * es,
-                                    (size_t)n, hipMemcpyHostToDevice, c->stream);
-        }));
-        CHK(stage_gram(c, dst, dtype, n, dl, dl, (double *)g->U[(size_t)r].p, pls[(size_t)r]));
+        CHK(stage_host_pipelined(c, src, ld, dtype, nullptr, 0, 0, n, dl, (char *)g->X[(size_t)r].p,
+                                 dl, (double *)g->U[(size_t)r].p, pls[(size_t)r]));
     }
     // 2. the exchange
     if (g->mode == BK_GROUP_ALLREDUCE) {
