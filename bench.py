@@ -426,6 +426,42 @@ def main():
             "parity": EMU_NOTE if emu else golden_check("D_512x1M_f256", sel2.cpu().numpy(),
                                                         mean[:dl].cpu().numpy(), c0, dl)}
 
+    if w["dtype"] == "f32":
+        # config E's "fp32 MFMA path" (bk_set_f32_mode BK_F32_MFMA): the same batch
+        # on v_mfma_f32_16x16x4_f32, fp32 accumulation per K1 segment
+        eng.set_f32_mode(_lib.BK_F32_MFMA)
+        step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        k2 = max(3, a.steps // 4)
+        eng.timing_select(["k_gram"])
+        t0 = time.perf_counter()
+        for _ in range(k2):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        e2 = time.perf_counter() - t0
+        kt2 = eng.timing_read()
+        if world > 1:
+            tt = torch.tensor([e2], dtype=torch.float64, device=dev)
+            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+            e2 = float(tt.item())
+        g2 = kt2.get("k_gram", {"avg_ms": float("nan")})
+        variants["f32_mfma"] = {
+            "what": "fp32 rows on the fp32 MFMA (tolerance re-stated, SURVEY §8(d))",
+            "steps": k2, "ms_per_step": round(e2 / k2 * 1e3, 4),
+            "value": round(n * (dl if emu else d) * es / (e2 / k2) / 1e9, 3),
+            "k_gram_ms": round(g2["avg_ms"], 4),
+            "k_gram_tflops": round(n * (n + 1) * dl / (g2["avg_ms"] * 1e-3) / 1e12, 2),
+            "k_gram_frac_of_fp32_peak": round(n * (n + 1) * dl / (g2["avg_ms"] * 1e-3) / 1e12
+                                              / PEAK_TFLOPS["f32"], 4),
+            "parity": EMU_NOTE if emu else golden_check(a.workload, sel.cpu().numpy(),
+                                                        mean[:dl].cpu().numpy(), c0, dl)}
+        eng.set_f32_mode(_lib.BK_F32_EXACT)
+        eng.timing_select([])
+
     # roofline of the dominant kernel (K1, fp64 MFMA): algorithmic flops per
     # launch = n(n+1) * d_local (symmetric Gram incl. diagonal)
     g = kt.get("k_gram", {"avg_ms": float("nan")})

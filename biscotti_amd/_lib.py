@@ -16,7 +16,8 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
-BK_ABI_VERSION = 5
+BK_ABI_VERSION = 6
+BK_F32_EXACT, BK_F32_MFMA = 0, 1
 KERNELS = ["k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni"]
 K = {name: i for i, name in enumerate(KERNELS)}
@@ -53,6 +54,7 @@ SIGNATURES = {
                                   _d, _i]),
     "bk_timing_enable": (_i, [_p, _i]),
     "bk_graph_enable": (_i, [_p, _i]),
+    "bk_set_f32_mode": (_i, [_p, _i]),
     "bk_timing_select": (_i, [_p, ctypes.c_uint32]),
     "bk_timing_read": (_i, [_p, _i, _pd, _pi64]),
     "bk_kernel_name": (ctypes.c_char_p, [_i]),

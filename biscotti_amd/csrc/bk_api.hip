@@ -108,6 +108,7 @@ struct bk_ctx {
     std::vector<CachedPlan> plans;
     int gram_variant = 3;  // 3: LDS-shared v3 for aligned fp64; 1: v1 everywhere (BK_GRAM=v1)
     int gram_mode = 0;     // BK_GRAM_MODE: timing-only ablations of v3 (tools/, never tests)
+    int f32_mode = BK_F32_EXACT;  // fp32 rows: widened onto the fp64 MFMA, or the fp32 MFMA
     // hipGraph replay of bk_multikrum_device (bk_graph_enable): one captured
     // launch sequence per call signature; every workspace reallocation or plan
     // eviction bumps ws_epoch, which retires the graphs that baked the old
@@ -333,7 +334,7 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
         }
         CHK(timed(c, BK_K_GRAM, [&] {
             return launch_gram3(dX, dtype, ld, (int)n, d, P3, part, c->stream, c->gram_mode,
-                                trace);
+                                trace, c->f32_mode == BK_F32_MFMA);
         }));
         if (tfile) {
             std::vector<long long> h((size_t)P3.nwg * 24);
@@ -716,6 +717,15 @@ int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t
     if (c->graph_on && c->timing == 0 && !getenv("BK_TRACE_FILE"))
         return run_device_graph(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
     return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
+}
+
+int bk_set_f32_mode(bk_ctx *c, int mode) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    if (mode != BK_F32_EXACT && mode != BK_F32_MFMA) return fail(BK_EINVAL, "bad f32 mode %d", mode);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->f32_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
+    c->f32_mode = mode;
+    return BK_OK;
 }
 
 int bk_graph_enable(bk_ctx *c, int on) {

@@ -73,7 +73,13 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk = G3_BK);
 // K1 v3: one launched workgroup runs its segments one after the other (a CU's
 // share of the columns may span two groups: bk_plan.hip "McNaughton")
 hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl,
-                        double *part, hipStream_t st, int mode = 0, long long *trace = nullptr);
+                        double *part, hipStream_t st, int mode = 0, long long *trace = nullptr,
+                        bool f32_mfma = false);
+// fp32 rows for the fp32-MFMA K1 (a distinct element type selects the kernel)
+struct f32m {
+    float v;
+    __host__ __device__ operator double() const { return v; }
+};
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st);
 hipError_t configure_kernels();
 hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan &pl,

@@ -261,19 +261,53 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // LDS image, swizzle and glds shape are the same for both input types.
 template <typename T>
 struct G3T;
+// op / acc: MFMA operand and accumulator types; F32C: the fp32 MFMA, whose
+// C/D map is row = 4*(lane>>4) + reg (the f64 one is (lane>>4) + 4*reg)
 template <>
 struct G3T<double> {
     typedef d2v gran;
+    typedef double op;
+    typedef d4v acc;
     static constexpr int SUB = 2;   // MFMA sub-steps (k=4 each) per granule
+    static constexpr bool F32C = false;
     static __device__ __forceinline__ double at(const d2v &v, int s) { return v[s]; }
+    static __device__ __forceinline__ d4v mma(double a, double b, d4v c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
 };
 template <>
 struct G3T<float> {
     typedef f4v gran;
+    typedef double op;
+    typedef d4v acc;
     static constexpr int SUB = 4;
+    static constexpr bool F32C = false;
     // fp32 -> fp64 is exact, and so is every fp32 x fp32 product in fp64
     static __device__ __forceinline__ double at(const f4v &v, int s) { return (double)v[s]; }
+    static __device__ __forceinline__ d4v mma(double a, double b, d4v c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
 };
+// fp32 rows on the fp32 MFMA (bk_set_f32_mode(ctx, BK_F32_MFMA), config E's
+// "fp32 MFMA path"): products rounded to fp32 and summed in fp32 within one
+// workgroup segment; the segments' partial slabs are summed in fp64 (K1b)
+template <>
+struct G3T<f32m> {
+    typedef f4v gran;
+    typedef float op;
+    typedef f4v acc;
+    static constexpr int SUB = 4;
+    static constexpr bool F32C = true;
+    static __device__ __forceinline__ float at(const f4v &v, int s) { return v[s]; }
+    static __device__ __forceinline__ f4v mma(float a, float b, f4v c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+};
+// output row of accumulator register r of lane group g in a 16x16 block
+template <typename T>
+__device__ __forceinline__ constexpr int g3_crow(int g, int r) {
+    return G3T<T>::F32C ? 4 * g + r : g + 4 * r;
+}
 
 template <typename T>
 __device__ __forceinline__ typename G3T<T>::gran g3_frag(const char *lds_blk, int q, int h, int rr,
@@ -317,24 +351,25 @@ __device__ __forceinline__ void g3_barrier() {
 // diagonal sub-tile: upper 16x16 blocks (i <= j) in a flat array of 10
 __device__ __forceinline__ constexpr int dix(int i, int j) { return i * 4 - i * (i - 1) / 2 + (j - i); }
 
-template <int KIND>
+template <int KIND, typename V>
 struct G3Acc;
-template <>
-struct G3Acc<T_OFF> {
-    d4v a[4][4];
+template <typename V>
+struct G3Acc<T_OFF, V> {
+    V a[4][4];
 };
-template <>
-struct G3Acc<T_PAIR> {
-    d4v a[10], b[10];
+template <typename V>
+struct G3Acc<T_PAIR, V> {
+    V a[10], b[10];
 };
-template <>
-struct G3Acc<T_DIAG1> {
-    d4v a[10];
+template <typename V>
+struct G3Acc<T_DIAG1, V> {
+    V a[10];
 };
 
 // SKIP: leave block (0,3) to the OFF wave that took it (balanced band quads)
-template <bool SKIP = false>
-__device__ __forceinline__ void diag_mma(d4v (&acc)[10], const d2v (&a)[4]) {
+template <typename T, bool SKIP = false>
+__device__ __forceinline__ void diag_mma(typename G3T<T>::acc (&acc)[10], const d2v (&a)[4]) {
+    typedef typename G3T<T>::op O;
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -342,15 +377,28 @@ __device__ __forceinline__ void diag_mma(d4v (&acc)[10], const d2v (&a)[4]) {
 #pragma unroll
             for (int j = i; j < 4; ++j) {
                 if (SKIP && i == 0 && j == 3) continue;
-                acc[dix(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][s], a[j][s], acc[dix(i, j)], 0, 0, 0);
+                acc[dix(i, j)] = G3T<T>::mma((O)a[i][s], (O)a[j][s], acc[dix(i, j)]);
             }
+}
+// the ragged-tail OFF product from direct loads (values exact in op)
+template <typename T>
+__device__ __forceinline__ void off_mma_tail(typename G3T<T>::acc (&acc)[4][4], const d2v (&a)[4],
+                                             const d2v (&b)[4]) {
+    typedef typename G3T<T>::op O;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = G3T<T>::mma((O)a[i][s], (O)b[j][s], acc[i][j]);
 }
 // the same over one granule of either input type
 template <typename T, bool SKIP = false>
-__device__ __forceinline__ void diag_mma_g(d4v (&acc)[10], const typename G3T<T>::gran (&a)[4]) {
+__device__ __forceinline__ void diag_mma_g(typename G3T<T>::acc (&acc)[10],
+                                           const typename G3T<T>::gran (&a)[4]) {
 #pragma unroll
     for (int s = 0; s < G3T<T>::SUB; ++s) {
-        double v[4];
+        typename G3T<T>::op v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = G3T<T>::at(a[i], s);
 #pragma unroll
@@ -358,7 +406,7 @@ __device__ __forceinline__ void diag_mma_g(d4v (&acc)[10], const typename G3T<T>
 #pragma unroll
             for (int j = i; j < 4; ++j) {
                 if (SKIP && i == 0 && j == 3) continue;
-                acc[dix(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[i], v[j], acc[dix(i, j)], 0, 0, 0);
+                acc[dix(i, j)] = G3T<T>::mma(v[i], v[j], acc[dix(i, j)]);
             }
     }
 }
@@ -375,17 +423,21 @@ __device__ __forceinline__ void g3_load_rows(d2v (&a)[4], const T *__restrict__ 
     }
 }
 
-__device__ __forceinline__ void store_tile(double *out, const d4v (&acc)[4][4], int rr, int g) {
+template <typename T = double>
+__device__ __forceinline__ void store_tile(double *out, const typename G3T<T>::acc (&acc)[4][4],
+                                           int rr, int g) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = acc[i][j][r];
+            for (int r = 0; r < 4; ++r)
+                out[(i * 16 + g3_crow<T>(g, r)) * 64 + j * 16 + rr] = (double)acc[i][j][r];
 }
 
-template <bool SKIP = false>
-__device__ __forceinline__ void store_diag(double *out, const d4v (&acc)[10], int rr, int g) {
+template <typename T, bool SKIP = false>
+__device__ __forceinline__ void store_diag(double *out, const typename G3T<T>::acc (&acc)[10],
+                                           int rr, int g) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -393,7 +445,8 @@ __device__ __forceinline__ void store_diag(double *out, const d4v (&acc)[10], in
             if (SKIP && i == 0 && j == 3) continue;  // written by the OFF wave that took it
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                out[(i * 16 + g + 4 * r) * 64 + j * 16 + rr] = j >= i ? acc[dix(i, j)][r] : 0.0;
+                out[(i * 16 + g3_crow<T>(g, r)) * 64 + j * 16 + rr] =
+                    j >= i ? (double)acc[dix(i, j)][r] : 0.0;
         }
 }
 
@@ -401,9 +454,11 @@ __device__ __forceinline__ void store_diag(double *out, const d4v (&acc)[10], in
 // tile; XT = 1 / 2: also block (0,3) of the diagonal tile of the A / B row-block
 // (operands already in registers: fragments 0 and 3 of that side)
 template <typename T, int S, int XT = 0>
-__device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const typename G3T<T>::gran (&a)[4],
-                                        const typename G3T<T>::gran (&b)[4], d4v &x) {
-    double va[4], vb[4];
+__device__ __forceinline__ void off_mma(typename G3T<T>::acc (&acc)[4][4],
+                                        const typename G3T<T>::gran (&a)[4],
+                                        const typename G3T<T>::gran (&b)[4],
+                                        typename G3T<T>::acc &x) {
+    typename G3T<T>::op va[4], vb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         va[i] = G3T<T>::at(a[i], S);
@@ -413,14 +468,16 @@ __device__ __forceinline__ void off_mma(d4v (&acc)[4][4], const typename G3T<T>:
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[i], vb[j], acc[i][j], 0, 0, 0);
-    if constexpr (XT == 1) x = __builtin_amdgcn_mfma_f64_16x16x4f64(va[0], va[3], x, 0, 0, 0);
-    if constexpr (XT == 2) x = __builtin_amdgcn_mfma_f64_16x16x4f64(vb[0], vb[3], x, 0, 0, 0);
+            acc[i][j] = G3T<T>::mma(va[i], vb[j], acc[i][j]);
+    if constexpr (XT == 1) x = G3T<T>::mma(va[0], va[3], x);
+    if constexpr (XT == 2) x = G3T<T>::mma(vb[0], vb[3], x);
 }
 // all SUB sub-steps of one granule
 template <typename T, int XT = 0>
-__device__ __forceinline__ void off_mma_gran(d4v (&acc)[4][4], const typename G3T<T>::gran (&a)[4],
-                                             const typename G3T<T>::gran (&b)[4], d4v &x) {
+__device__ __forceinline__ void off_mma_gran(typename G3T<T>::acc (&acc)[4][4],
+                                             const typename G3T<T>::gran (&a)[4],
+                                             const typename G3T<T>::gran (&b)[4],
+                                             typename G3T<T>::acc &x) {
     off_mma<T, 0, XT>(acc, a, b, x);
     off_mma<T, 1, XT>(acc, a, b, x);
     if constexpr (G3T<T>::SUB == 4) {
@@ -536,20 +593,21 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
                                                  (void *)(base + gdst[m]), 16, 0, 0);
     };
 
-    G3Acc<KIND == T_NONE ? T_DIAG1 : KIND> acc;
+    typedef typename G3T<T>::acc AV;
+    G3Acc<KIND == T_NONE ? T_DIAG1 : KIND, AV> acc;
     if constexpr (KIND == T_OFF) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc.a[i][j] = d4v{0.0, 0.0, 0.0, 0.0};
+            for (int j = 0; j < 4; ++j) acc.a[i][j] = AV{0, 0, 0, 0};
     } else if constexpr (KIND == T_PAIR) {
 #pragma unroll
-        for (int i = 0; i < 10; ++i) acc.a[i] = acc.b[i] = d4v{0.0, 0.0, 0.0, 0.0};
+        for (int i = 0; i < 10; ++i) acc.a[i] = acc.b[i] = AV{0, 0, 0, 0};
     } else if constexpr (KIND == T_DIAG1) {
 #pragma unroll
-        for (int i = 0; i < 10; ++i) acc.a[i] = d4v{0.0, 0.0, 0.0, 0.0};
+        for (int i = 0; i < 10; ++i) acc.a[i] = AV{0, 0, 0, 0};
     }
-    d4v xacc = d4v{0.0, 0.0, 0.0, 0.0};  // XO: the extra diagonal block
+    AV xacc = AV{0, 0, 0, 0};  // XO: the extra diagonal block
     gran ha[4], hb[4];  // STAG: the held second granule of the previous k-block
 #pragma unroll
     for (int q = 0; q < 4; ++q) ha[q] = hb[q] = gran{};
@@ -654,33 +712,32 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
                 g3_load_rows<T>(a, X, ld, n, blk[sA], cc, d, rr);
                 g3_load_rows<T>(b, X, ld, n, blk[sB], cc, d, rr);
                 if constexpr (KIND == T_OFF) {
-                    gram_mma<false>(acc.a, a, b);
+                    typedef typename G3T<T>::op O;
+                    off_mma_tail<T>(acc.a, a, b);
 #pragma unroll
                     for (int s2 = 0; s2 < 2; ++s2) {
-                        if constexpr (XO == 1)
-                            xacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0][s2], a[3][s2], xacc, 0, 0, 0);
-                        if constexpr (XO == 2)
-                            xacc = __builtin_amdgcn_mfma_f64_16x16x4f64(b[0][s2], b[3][s2], xacc, 0, 0, 0);
+                        if constexpr (XO == 1) xacc = G3T<T>::mma((O)a[0][s2], (O)a[3][s2], xacc);
+                        if constexpr (XO == 2) xacc = G3T<T>::mma((O)b[0][s2], (O)b[3][s2], xacc);
                     }
                 } else if constexpr (KIND == T_PAIR) {
-                    diag_mma<XP>(acc.a, a);
-                    diag_mma<XP>(acc.b, b);
+                    diag_mma<T, XP>(acc.a, a);
+                    diag_mma<T, XP>(acc.b, b);
                 } else {
-                    diag_mma(acc.a, a);
+                    diag_mma<T>(acc.a, a);
                 }
             }
         }
         if constexpr (KIND == T_OFF) {
-            store_tile(out, acc.a, rr, g);
+            store_tile<T>(out, acc.a, rr, g);
             if constexpr (XO != 0) {  // block (0,3) of the PAIR wave's diagonal tile
 #pragma unroll
-                for (int r = 0; r < 4; ++r) xout[(g + 4 * r) * 64 + 48 + rr] = xacc[r];
+                for (int r = 0; r < 4; ++r) xout[g3_crow<T>(g, r) * 64 + 48 + rr] = (double)xacc[r];
             }
         } else if constexpr (KIND == T_PAIR) {
-            store_diag<XP>(out, acc.a, rr, g);
-            store_diag<XP>(out + 4096, acc.b, rr, g);
+            store_diag<T, XP>(out, acc.a, rr, g);
+            store_diag<T, XP>(out + 4096, acc.b, rr, g);
         } else {
-            store_diag(out, acc.a, rr, g);
+            store_diag<T>(out, acc.a, rr, g);
         }
     }
 }
@@ -1262,10 +1319,13 @@ hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, i
 }
 
 hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl,
-                        double *part, hipStream_t st, int mode, long long *trace) {
+                        double *part, hipStream_t st, int mode, long long *trace, bool f32_mfma) {
     // mode != 0: timing-only ablations (1: no MFMA, 2: no global loads) -- wrong results
     const dim3 grid((unsigned)pl.nwg), block(512);
-    if (dtype != 0)  // fp32 input: production mode only
+    if (dtype != 0 && f32_mfma)  // fp32 input on the fp32 MFMA
+        hipLaunchKernelGGL((k_gram3<0, f32m>), grid, block, G3_LDS, st, (const f32m *)X, ld, n,
+                           pl.nfull, d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
+    else if (dtype != 0)  // fp32 input, exact (widened onto the fp64 MFMA): production mode only
         hipLaunchKernelGGL((k_gram3<0, float>), grid, block, G3_LDS, st, (const float *)X, ld, n,
                            pl.nfull, d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
     else if (mode == 1)
@@ -1293,7 +1353,8 @@ hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStr
 
 hipError_t configure_kernels() {
     for (const void *k : {(const void *)k_gram3<0>, (const void *)k_gram3<1>,
-                          (const void *)k_gram3<2>, (const void *)k_gram3<0, float>}) {
+                          (const void *)k_gram3<2>, (const void *)k_gram3<0, float>,
+                          (const void *)k_gram3<0, f32m>}) {
         hipError_t e0 = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
         if (e0 != hipSuccess) return e0;
     }

@@ -274,6 +274,11 @@ class Engine:
     def timing_enable(self, on=True):
         check(lib().bk_timing_enable(self._ctx, 1 if on else 0))
 
+    def set_f32_mode(self, mode):
+        """_lib.BK_F32_EXACT (fp32 rows widened onto the fp64 MFMA, default) or
+        _lib.BK_F32_MFMA (the fp32 MFMA, fp32 accumulation per K1 segment)."""
+        check(lib().bk_set_f32_mode(self._ctx, int(mode)))
+
     def graph_enable(self, on=True):
         """Replay multikrum_device_ptr calls as hipGraphs (bk_graph_enable)."""
         check(lib().bk_graph_enable(self._ctx, 1 if on else 0))

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 5
+#define BK_ABI_VERSION 6
 
 typedef struct bk_ctx bk_ctx;
 
@@ -103,6 +103,18 @@ int bk_multikrum_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64
  * bypassed while per-kernel timing is on, and retired when the context's
  * workspace is reallocated.  Off by default; on = 0 frees the cached graphs. */
 int bk_graph_enable(bk_ctx *ctx, int on);
+
+/* fp32 rows (dtype BK_F32): BK_F32_EXACT (default) widens every element onto
+ * the fp64 MFMA, which is exact per product and accumulates in fp64.
+ * BK_F32_MFMA (BASELINE config E's "fp32 MFMA path") runs
+ * v_mfma_f32_16x16x4_f32 at twice the fp64 rate: products are rounded to fp32
+ * and summed in fp32 within one K1 workgroup segment, and the segments'
+ * partials are summed in fp64.  Tolerance, as SURVEY.md §8(d) restates it for
+ * config E: the selection matches wherever the score gap at the boundary
+ * exceeds the fp32 Gram error bound (~2 k gamma_d max|x_i|^2).  The mean is
+ * unchanged (fp64 accumulation of the fp32 rows).  No effect on fp64 rows. */
+enum bk_f32_mode { BK_F32_EXACT = 0, BK_F32_MFMA = 1 };
+int bk_set_f32_mode(bk_ctx *ctx, int mode);
 
 /* ---- dimension-sharded stages (one process / device per column shard) ----
  * Packed upper-triangle Gram: bk_upper_elems(n) doubles.  Summing the packed
