@@ -396,7 +396,7 @@ int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
 // after K6 when noise is applied) runs on the compute stream while the next
 // chunk is in flight.  The Gram is additive over columns, so only the last
 // chunk's K1 and the finish remain after the copies; the chunk partials are
-// summed in chunk order (deterministic).  Noise: vector j of update i at
+// added to a running sum in chunk order (deterministic).  Noise: vector j of update i at
 // noise + (i*k + j) * noise_ld, staged per chunk in a 2-slot device ring.
 // On return (async) the device batch dX (row stride dld) is complete and
 // noised and U holds the full packed Gram; pl describes it for stage_finish.
@@ -414,16 +414,18 @@ int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const 
     int64_t cap = (int64_t)256 << 20;
     if (const char *v = getenv("BK_STAGE_CHUNK_BYTES")) cap = atoll(v) > 0 ? atoll(v) : cap;
     const int64_t col_bytes = n * (int64_t)es + n * k * (int64_t)sizeof(double);
+    // at most 64 chunks: every chunk writes and adds one packed partial Gram
+    // (n^2/2 doubles: 1 GiB at n = 16384), which must stay small against its copy
     int64_t W = cap / col_bytes;
-    W = W < 64 ? 64 : W / 64 * 64;
+    W = W < (d + 63) / 64 ? (d + 63) / 64 : W;
+    W = W < 64 ? 64 : (W + 63) / 64 * 64;
     if (W >= d) W = d;
     const int64_t C = (d + W - 1) / W;
-    if (C > 1024) return fail(BK_EINVAL, "BK_STAGE_CHUNK_BYTES too small (%lld chunks)", (long long)C);
     const size_t usz = (size_t)bk_upper_elems(n);
-    double *Ug = U;
+    double *P = nullptr;
     if (C > 1) {
-        CHK(ensure(c->Ug, usz * C * sizeof(double)));
-        Ug = (double *)c->Ug.p;
+        CHK(ensure(c->Ug, usz * sizeof(double)));
+        P = (double *)c->Ug.p;
     }
     double *ring = nullptr;
     if (k > 0) {
@@ -454,9 +456,10 @@ int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const 
             }));
             HIPCHK(hipEventRecord(c->ev_use[s], c->stream));
         }
-        CHK(stage_gram(c, dX + c0 * es, dtype, n, wc, dld, Ug + (size_t)ch * usz, pl));
+        // chunk 0 straight into U, later chunks added in chunk order
+        CHK(stage_gram(c, dX + c0 * es, dtype, n, wc, dld, ch == 0 ? U : P, pl));
+        if (ch > 0) HIPCHK(launch_add_upper(U, P, (int64_t)usz, c->stream));
     }
-    if (C > 1) HIPCHK(launch_sum_ranks(Ug, (int)C, (int64_t)usz, U, c->stream));
     pl.d = d;
     return BK_OK;
 }

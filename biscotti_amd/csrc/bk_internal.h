@@ -86,6 +86,7 @@ hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, c
                        double *part, hipStream_t st);
 hipError_t launch_reduce(const double *part, const Plan &pl, double *U, hipStream_t st);
 hipError_t launch_sum_ranks(const double *Ug, int R, int64_t stride, double *U, hipStream_t st);
+hipError_t launch_add_upper(double *U, const double *P, int64_t count, hipStream_t st);
 hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores,
                          hipStream_t st);
 hipError_t launch_rank(const double *scores, int n, int m, int *mask, hipStream_t st);

@@ -1219,6 +1219,25 @@ hipError_t launch_reduce(const double *part, const Plan &pl, double *U, hipStrea
     return hipGetLastError();
 }
 
+// U[e] += P[e]: the host entries' running sum of column-chunk Gram partials
+// (chunk order, so deterministic)
+__global__ __launch_bounds__(256) void k_add_upper(double *__restrict__ U,
+                                                   const double *__restrict__ P, int64_t count) {
+    const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (e + 1 < count) {
+        d2v u = *reinterpret_cast<const d2v *>(U + e), p = *reinterpret_cast<const d2v *>(P + e);
+        *reinterpret_cast<d2v *>(U + e) = u + p;
+    } else if (e < count) {
+        U[e] += P[e];
+    }
+}
+
+hipError_t launch_add_upper(double *U, const double *P, int64_t count, hipStream_t st) {
+    hipLaunchKernelGGL(k_add_upper, dim3((unsigned)((count + 511) / 512)), dim3(256), 0, st, U, P,
+                       count);
+    return hipGetLastError();
+}
+
 hipError_t launch_sum_ranks(const double *Ug, int R, int64_t stride, double *U, hipStream_t st) {
     hipLaunchKernelGGL(k_sum_ranks, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, st, Ug, R,
                        stride, U);

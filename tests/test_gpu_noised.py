@@ -119,7 +119,7 @@ def test_noised_repeated_calls_and_errors(engine, oracle):
 @pytest.mark.parametrize("n,d,f,dtype,chunk_cols", [
     (512, 65536, 153, "f64", 4096),   # 16 chunks
     (100, 7850, 30, "f64", 1024),     # ragged last chunk
-    (64, 9001, 19, "f64", 64),        # odd d, 141 chunks
+    (64, 9001, 19, "f64", 64),        # odd d, 47 chunks (the 64-chunk cap)
     (96, 20000, 28, "f32", 2048),     # fp32 rows
 ])
 def test_host_entry_chunked_vs_device(engine, oracle, monkeypatch, n, d, f, dtype, chunk_cols):
