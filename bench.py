@@ -422,7 +422,7 @@ def main():
             e2 = float(tt.item())
         variants["D_512x1M_f256"] = {
             "f": f2, "m": n - f2, "steps": k2, "ms_per_step": round(e2 / k2 * 1e3, 4),
-            "value": round(n * d * es / (e2 / k2) / 1e9, 3),
+            "value": round(n * (dl if emu else d) * es / (e2 / k2) / 1e9, 3),
             "parity": EMU_NOTE if emu else golden_check("D_512x1M_f256", sel2.cpu().numpy(),
                                                         mean[:dl].cpu().numpy(), c0, dl)}
 
