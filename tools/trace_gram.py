@@ -5,7 +5,9 @@ records 100 MHz start/end, shader-clock start/end, HW_ID, XCC_ID) and reports:
   * loop efficiency  = ideal MFMA cycles (nk * cost * 256) / measured cycles
   * fill efficiency  = sum of WG busy time / (CUs * makespan)
   * the distribution of per-WG durations per group.
-Env: N, D, MODES (comma list of BK_GRAM_MODE values, default "0,2").
+Env: N, D, MODES (comma list of BK_GRAM_MODE values, default "0,2"); DTYPE=f32
+for fp32 rows, with F32MFMA=1 on the fp32 MFMA (bk_set_f32_mode) -- its ideal
+per k-block is the same cost * 256 cycles (8 MFMAs of 32 cycles per 32 columns).
 """
 import collections
 import os
@@ -25,19 +27,23 @@ from biscotti_amd.krum import Engine  # noqa: E402
 
 n, d = int(os.environ.get("N", 512)), int(os.environ.get("D", 1 << 20))
 modes = os.environ.get("MODES", "0,2").split(",")
-X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+f32 = os.environ.get("DTYPE") == "f32"
+dt = _lib.BK_F32 if f32 else _lib.BK_F64
+X = torch.empty((n, d), dtype=torch.float32 if f32 else torch.float64, device="cuda")
 U = torch.empty(int(_lib.lib().bk_upper_elems(n)), dtype=torch.float64, device="cuda")
 for mode in modes:
     os.environ["BK_GRAM_MODE"] = mode
     e = Engine(0)
     os.environ.pop("BK_GRAM_MODE")
-    e.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 1, n // 3)
+    if os.environ.get("F32MFMA") == "1":
+        e.set_f32_mode(_lib.BK_F32_MFMA)
+    e.synth_fill_ptr(X.data_ptr(), dt, n, d, d, 0, d, 1, n // 3)
     for _ in range(3):
-        e.gram_upper_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, U.data_ptr())
+        e.gram_upper_ptr(X.data_ptr(), dt, n, d, d, U.data_ptr())
     e.synchronize()
     fn = tempfile.mktemp(suffix=".bin")
     os.environ["BK_TRACE_FILE"] = fn
-    e.gram_upper_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, U.data_ptr())
+    e.gram_upper_ptr(X.data_ptr(), dt, n, d, d, U.data_ptr())
     e.synchronize()
     os.environ.pop("BK_TRACE_FILE")
     tr = np.fromfile(fn, dtype=np.int64).reshape(-1, 24)
