@@ -539,7 +539,9 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
 #ifndef BK_GLDS_E4
 #define BK_GLDS_E4 2
 #endif
-    constexpr int ESPL = NB == 6 ? BK_GLDS_E6 : NB == 4 ? BK_GLDS_E4 : 0;
+    // the fp32-MFMA kernel runs unstaggered, so its waves split evenly (the
+    // uneven split put the band quads' loop at 0.65 there, even 0.905)
+    constexpr int ESPL = G3T<T>::F32C ? 0 : NB == 6 ? BK_GLDS_E6 : NB == 4 ? BK_GLDS_E4 : 0;
     constexpr int CLO = NB + ESPL, CHI = NB - ESPL;
     constexpr int GMAX = G3_MAXB + 2;
     static_assert(CLO <= GMAX && CHI >= 0, "glds split exceeds the per-wave pointer table");
