@@ -761,7 +761,10 @@ __device__ __forceinline__ void g3_dispatch(const T *__restrict__ X, int64_t ld,
         // the stagger covers the fp64 MFMA's 64-cycle issue; on the fp32 MFMA
         // (32 cycles) it costs more than it hides: E's loop efficiency 0.776
         // staggered, 0.845 not (tools/trace_gram.py)
-        if (wave >= 4 && G3_STAGGER && !G3T<T>::F32C) {
+#ifndef BK_F32_STAGGER  // probe knob: 1 staggers the fp32-MFMA kernel too
+#define BK_F32_STAGGER 0
+#endif
+        if (wave >= 4 && G3_STAGGER && (!G3T<T>::F32C || BK_F32_STAGGER)) {
             if (xt == 1)
                 g3_wave<T, T_OFF, MODE, true, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
             else if (xt == 2)
