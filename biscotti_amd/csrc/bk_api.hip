@@ -391,6 +391,18 @@ int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
     return stage_finish(c, U, pl, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
 }
 
+// Error paths of the host entries: queued H2D copies may still read the
+// caller's buffers, so both streams are drained unless the entry disarms this.
+struct HostDrain {
+    bk_ctx *c;
+    bool armed = true;
+    ~HostDrain() {
+        if (!armed) return;
+        if (c->copy) (void)hipStreamSynchronize(c->copy);
+        (void)hipStreamSynchronize(c->stream);
+    }
+};
+
 // Host entries (bk_multikrum, bk_multikrum_noised): the batch crosses PCIe in
 // column chunks on a copy stream, and each chunk's partial Gram (K1 + K1b,
 // after K6 when noise is applied) runs on the compute stream while the next
@@ -432,6 +444,9 @@ int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const 
         CHK(ensure(c->noise, (size_t)2 * n * k * W * sizeof(double)));
         ring = (double *)c->noise.p;
     }
+    // on an error return, copies already queued may still read the caller's
+    // host buffers: drain both streams before handing control back
+    HostDrain drain{c};
     // earlier work on the compute stream may still read the batch / the ring
     HIPCHK(hipEventRecord(c->ev_go, c->stream));
     HIPCHK(hipStreamWaitEvent(c->copy, c->ev_go, 0));
@@ -461,6 +476,7 @@ int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const 
         if (ch > 0) HIPCHK(launch_add_upper(U, P, (int64_t)usz, c->stream));
     }
     pl.d = d;
+    drain.armed = false;
     return BK_OK;
 }
 
@@ -469,6 +485,7 @@ int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const 
 int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t dld,
                      int64_t f, const double *U, const Plan &pl, int64_t *sel_idx,
                      int64_t *m_out, double *scores, double *mean_out) {
+    HostDrain drain{c};
     const int64_t m = n - f;
     CHK(ensure(c->sel, (size_t)n * sizeof(int64_t)));
     CHK(ensure(c->scores, (size_t)n * sizeof(double)));
@@ -489,6 +506,7 @@ int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
         return e;
     }));
     HIPCHK(hipStreamSynchronize(c->stream));
+    drain.armed = false;
     if (m_out) *m_out = m;
     return BK_OK;
 }
