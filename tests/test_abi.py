@@ -111,6 +111,9 @@ def test_null_and_bad_arguments_do_not_crash():
                                 None) == _lib.BK_EINVAL
     assert L.bk_group_size(None) == 0 and L.bk_group_ctx(None, 0) is None
     L.bk_group_destroy(None)
+    assert L.bk_set_f32_mode(None, _lib.BK_F32_MFMA) == _lib.BK_EINVAL
+    assert L.bk_multikrum_noised(None, None, 10, None, 1, 10, _lib.BK_HOST, 10, 10, 2, None, None,
+                                 None, None, None, 10) == _lib.BK_EINVAL
 
 
 def test_no_gpu_fails_loudly():
