@@ -16,8 +16,8 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
-BK_ABI_VERSION = 6
-BK_F32_EXACT, BK_F32_MFMA = 0, 1
+BK_ABI_VERSION = 7
+BK_F32_EXACT, BK_F32_MFMA, BK_F32_CERTIFIED = 0, 1, 2
 KERNELS = ["k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni"]
 K = {name: i for i, name in enumerate(KERNELS)}
@@ -73,6 +73,11 @@ SIGNATURES = {
     "bk_group_size": (_i, [_p]),
     "bk_group_multikrum": (_i, [_p, _p, _i, _i, _i64, _i64, _i64, _i64, _p, _p, _p, _p]),
     "bk_group_ctx": (_p, [_p, _i]),
+    "bk_selection_margin": (_i, [_p, _pd, _pd, ctypes.POINTER(_i)]),
+    "bk_selection_margin_record": (_i, [_p, _pd]),
+    "bk_certified_reruns": (_i64, [_p]),
+    "bk_comm_size": (_i, [_p, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "bk_comm_stats": (_i, [_p, _pi64, _pd]),
 }
 
 _lib = None

@@ -78,6 +78,12 @@ struct bk_ctx {
     std::mutex mu;
     // workspace (grow-only)
     DevBuf part, U, Ug, scores, mask, sel, X, mean, perm, trace, idx;
+    // the selection margin of the last finish (K2 diag, K3 boundary scores, K3b record)
+    DevBuf diag, bnd, margin;
+    int margin_valid = 0;
+    // BK_F32_CERTIFIED: 1 while the exact re-run of a near-tie call is in progress
+    int force_exact = 0;
+    int64_t certified_reruns = 0;
     // RONI: the validation set (bk_roni_set_validation) and per-call scratch
     DevBuf roni_X, roni_y, roni_w, roni_d, roni_cnt, roni_s;
     int64_t roni_nv = 0, roni_dim = 0;
@@ -129,6 +135,8 @@ struct bk_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     int deterministic = 0;
+    int64_t exchanges = 0;        // exchanges of the packed Gram (bk_comm_stats)
+    double exchanged_bytes = 0;   // bytes each rank put into them
 };
 
 namespace {
@@ -164,7 +172,7 @@ void bind_epoch(bk_ctx *c) {
     DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,   &c->scores, &c->mask,   &c->sel,
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                      &c->noise};
+                      &c->noise, &c->diag, &c->bnd, &c->margin};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -312,7 +320,15 @@ bool use_v3(bk_ctx *c, const void *dX, int dtype, int64_t ld) {
 }
 int v3_bk(int dtype) { return dtype == BK_F64 ? G3_BK : 2 * G3_BK; }
 
-// K1 + K1b: packed upper-triangle Gram of this call's columns into U
+// fp32 rows on the fp32 MFMA for this call: BK_F32_MFMA, or BK_F32_CERTIFIED
+// unless its exact re-run of a near tie is in progress
+bool f32_mfma_now(const bk_ctx *c, int dtype) {
+    return dtype == BK_F32 && !c->force_exact &&
+           (c->f32_mode == BK_F32_MFMA || c->f32_mode == BK_F32_CERTIFIED);
+}
+
+// K1 + K1b: packed upper-triangle Gram of this call's columns into U (tiles,
+// then the trailing element = the column count, bk_upper_elems)
 int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
                double *U, Plan &pl) {
     if (use_v3(c, dX, dtype, ld)) {
@@ -334,7 +350,7 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
         }
         CHK(timed(c, BK_K_GRAM, [&] {
             return launch_gram3(dX, dtype, ld, (int)n, d, P3, part, c->stream, c->gram_mode,
-                                trace, c->f32_mode == BK_F32_MFMA);
+                                trace, f32_mfma_now(c, dtype));
         }));
         if (tfile) {
             std::vector<long long> h((size_t)P3.nwg * 24);
@@ -368,12 +384,25 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
         CHK(ensure(c->scores, (size_t)n * sizeof(double)));
         sc = (double *)c->scores.p;
     }
+    CHK(ensure(c->diag, (size_t)n * sizeof(double)));
+    CHK(ensure(c->bnd, 2 * sizeof(double)));
+    CHK(ensure(c->margin, 8 * sizeof(double)));
     int *mask = (int *)c->mask.p;
+    double *diag = (double *)c->diag.p, *bnd = (double *)c->bnd.p;
     const int64_t m = n - f;
     const int64_t k = n - f - 2 > 0 ? n - f - 2 : 0;
-    CHK(timed(c, BK_K_SCORES, [&] { return launch_scores(U, pl.T, (int)n, k, sc, c->stream); }));
-    CHK(timed(c, BK_K_RANK, [&] { return launch_rank(sc, (int)n, (int)m, mask, c->stream); }));
-    CHK(timed(c, BK_K_COMPACT, [&] { return launch_compact(mask, (int)n, d_sel, c->stream); }));
+    // unit roundoff of this Gram's accumulation (the margin's bound)
+    const double u_gram = f32_mfma_now(c, dtype) ? 0x1p-24 : 0x1p-53;
+    const double *dcols = U + (size_t)pl.ntile * 4096;  // the packed upper's trailing element
+    CHK(timed(c, BK_K_SCORES,
+              [&] { return launch_scores(U, pl.T, (int)n, k, sc, diag, c->stream); }));
+    CHK(timed(c, BK_K_RANK,
+              [&] { return launch_rank(sc, (int)n, (int)m, mask, bnd, c->stream); }));
+    CHK(timed(c, BK_K_COMPACT, [&] {
+        return launch_compact(mask, (int)n, d_sel, diag, bnd, dcols, k, u_gram,
+                              (double *)c->margin.p, c->stream);
+    }));
+    c->margin_valid = 1;
     if (d_mean && d > 0)
         CHK(timed(c, BK_K_MEAN, [&] {
             return launch_mean(dX, dtype, ld, d, d_sel, (int)m, d_mean, c->num_cu, c->stream);
@@ -384,7 +413,7 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
 int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld, int64_t f,
                int64_t *d_sel, double *d_scores, double *d_mean) {
     Plan pl;
-    const size_t usz = (size_t)((n + 63) / 64) * ((n + 63) / 64 + 1) / 2 * 4096;
+    const size_t usz = (size_t)bk_upper_elems(n);
     CHK(ensure(c->U, usz * sizeof(double)));
     double *U = (double *)c->U.p;
     CHK(stage_gram(c, dX, dtype, n, d, ld, U, pl));
@@ -417,9 +446,25 @@ int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const 
                          int64_t dld, double *U, Plan &pl) {
     const size_t es = esize(dtype);
     if (!c->copy) {
-        HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
-        for (hipEvent_t *ev : {&c->ev_go, &c->ev_cp[0], &c->ev_cp[1], &c->ev_use[0], &c->ev_use[1]})
-            HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        // create the copy stream and its five events into locals and publish
+        // them together: a half-built set would break every later host call
+        hipStream_t cs = nullptr;
+        hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+        hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+        for (int i = 0; i < 5 && e == hipSuccess; ++i)
+            e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            for (hipEvent_t x : ev)
+                if (x) (void)hipEventDestroy(x);
+            if (cs) (void)hipStreamDestroy(cs);
+            return fail(BK_EHIP, "copy stream / events: %s", hipGetErrorString(e));
+        }
+        c->copy = cs;
+        c->ev_go = ev[0];
+        c->ev_cp[0] = ev[1];
+        c->ev_cp[1] = ev[2];
+        c->ev_use[0] = ev[3];
+        c->ev_use[1] = ev[4];
     }
     // chunks of ~BK_STAGE_CHUNK_BYTES (default 256 MiB) of the batch plus its
     // noise; widths a multiple of 64 columns (16-B aligned chunk starts)
@@ -522,6 +567,38 @@ struct DeviceGuard {
     }
 };
 
+// the last finish's margin record (k_compact: gap, err_bound, near_tie, M,
+// s_lo, s_hi, d, k), synchronously
+int read_margin(bk_ctx *c, double (&mg)[8]) {
+    if (!c->margin_valid) return fail(BK_EINVAL, "no Multi-Krum call on this context yet");
+    HIPCHK(hipMemcpyAsync(mg, c->margin.p, sizeof mg, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BK_OK;
+}
+
+bool certified(const bk_ctx *c, int dtype) {
+    return dtype == BK_F32 && c->f32_mode == BK_F32_CERTIFIED;
+}
+
+// BK_F32_CERTIFIED: run on the fp32 MFMA; if the selection margin does not
+// clear the fp32 error bound, run again on the exact path (fp32 widened onto
+// the fp64 MFMA), whose outputs replace the first run's.  Synchronous (the
+// decision needs the margin on the host).  In the sharded entry every rank
+// holds the same summed Gram, hence the same margin and the same decision, so
+// the re-run's exchange is joined by all ranks.
+template <typename F>
+int run_certified(bk_ctx *c, F &&run) {
+    CHK(run());
+    double mg[8];
+    CHK(read_margin(c, mg));
+    if (mg[2] == 0.0) return BK_OK;
+    c->force_exact = 1;
+    const int st = run();
+    c->force_exact = 0;
+    if (st == BK_OK) ++c->certified_reruns;
+    return st;
+}
+
 }  // namespace
 
 extern "C" {
@@ -546,7 +623,7 @@ const char *bk_kernel_name(int kid) {
 
 int64_t bk_upper_elems(int64_t n) {
     const int64_t T = (n + 63) / 64;
-    return T * (T + 1) / 2 * 4096;
+    return T * (T + 1) / 2 * 4096 + 1;  // + the column count (K3b's margin)
 }
 
 int bk_create(bk_ctx **out, int device) {
@@ -593,7 +670,7 @@ void bk_destroy(bk_ctx *c) {
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->scores,
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                          &c->noise};
+                          &c->noise, &c->diag, &c->bnd, &c->margin};
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
@@ -735,6 +812,8 @@ int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t
     if (!d_sel) return fail(BK_EINVAL, "null d_sel_idx");
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
+    if (certified(c, dtype))
+        return run_certified(c, [&] { return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean); });
     if (c->graph_on && c->timing == 0 && !getenv("BK_TRACE_FILE"))
         return run_device_graph(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
     return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
@@ -742,7 +821,8 @@ int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t
 
 int bk_set_f32_mode(bk_ctx *c, int mode) {
     if (!c) return fail(BK_EINVAL, "null context");
-    if (mode != BK_F32_EXACT && mode != BK_F32_MFMA) return fail(BK_EINVAL, "bad f32 mode %d", mode);
+    if (mode != BK_F32_EXACT && mode != BK_F32_MFMA && mode != BK_F32_CERTIFIED)
+        return fail(BK_EINVAL, "bad f32 mode %d", mode);
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f32_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
     c->f32_mode = mode;
@@ -787,7 +867,23 @@ int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
     } else {
         CHK(stage_gram(c, dX, dtype, n, d, dld, U, pl));
     }
-    return run_host_outputs(c, dX, dtype, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out);
+    CHK(run_host_outputs(c, dX, dtype, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out));
+    if (certified(c, dtype)) {  // exact re-run of a near tie from the device-resident batch
+        double mg[8];
+        CHK(read_margin(c, mg));
+        if (mg[2] != 0.0) {
+            c->force_exact = 1;
+            Plan pl2;
+            int st = stage_gram(c, dX, dtype, n, d, dld, U, pl2);
+            if (st == BK_OK)
+                st = run_host_outputs(c, dX, dtype, n, d, dld, f, U, pl2, sel_idx, m_out, scores,
+                                      mean_out);
+            c->force_exact = 0;
+            if (st == BK_OK) ++c->certified_reruns;
+            return st;
+        }
+    }
+    return BK_OK;
 }
 
 // the noise application fused into the H2D staging of
@@ -817,13 +913,18 @@ int bk_multikrum_noised(bk_ctx *c, const double *delta, int64_t ld, const double
     CHK(ensure(c->U, (size_t)bk_upper_elems(n) * sizeof(double)));
     double *U = (double *)c->U.p;
     Plan pl;
+    // armed until the outputs have landed: on any error return, copies still
+    // queued may read delta / noise or write noised_out
+    HostDrain drain{c};
     // k = 0: no noisers, NoisedDelta = Delta (main.go:1599-1602)
     CHK(stage_host_pipelined(c, delta, ld, BK_F64, k > 0 ? noise : nullptr, k, noise_ld, n, d,
                              (char *)dX, dld, U, pl));
     if (noised_out)
         HIPCHK(hipMemcpy2DAsync(noised_out, (size_t)out_ld * 8, dX, (size_t)dld * 8,
                                 (size_t)d * 8, (size_t)n, hipMemcpyDeviceToHost, c->stream));
-    return run_host_outputs(c, dX, BK_F64, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out);
+    CHK(run_host_outputs(c, dX, BK_F64, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out));
+    drain.armed = false;
+    return BK_OK;
 }
 
 int bk_gram_upper_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
@@ -884,52 +985,117 @@ int bk_comm_set_mode(bk_ctx *c, int deterministic) {
     return BK_OK;
 }
 
-int bk_multikrum_sharded_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl,
-                                int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
-                                double *d_mean) {
-    CHK(check_common(c, dX, dtype, n, dl, ld));
-    CHK(bk_check_args(n, dl, f));
-    if (!d_sel) return fail(BK_EINVAL, "null d_sel_idx");
-    std::lock_guard<std::mutex> lk(c->mu);
-    DeviceGuard dg(c->device);
-    if (c->nranks > 1 && !c->comm) return fail(BK_ERCCL, "bk_comm_init not called");
+namespace {
+// one pass of the sharded entry: partial Gram of the local columns (zeros for
+// an empty shard), the exchange, then scores/selection and the local mean
+int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, int64_t ld,
+                 int64_t f, int64_t *d_sel, double *d_scores, double *d_mean) {
     const int64_t usz = bk_upper_elems(n);
     CHK(ensure(c->U, (size_t)usz * sizeof(double)));
     double *U = (double *)c->U.p;
     Plan pl;
-    CHK(stage_gram(c, dX, dtype, n, dl, ld, U, pl));
+    if (dl > 0) {
+        CHK(stage_gram(c, dX, dtype, n, dl, ld, U, pl));
+    } else {
+        // an empty column shard (d small against the rank count): a zero
+        // partial (column count 0 too), so this rank still joins the exchange
+        HIPCHK(hipMemsetAsync(U, 0, (size_t)usz * sizeof(double), c->stream));
+        pl.n = (int)n;
+        pl.T = (int)((n + 63) / 64);
+        pl.ntile = pl.T * (pl.T + 1) / 2;
+    }
     if (c->comm) {  // also at 1 rank, so the exchange is exercised on a 1-GPU box
+        hipEvent_t a = nullptr, b = nullptr;
+        if (timing_on(c, BK_K_ALLREDUCE)) {
+            CHK(get_event(c, &a));
+            CHK(get_event(c, &b));
+            HIPCHK(hipEventRecord(a, c->stream));
+        }
         if (!c->deterministic) {
-            hipEvent_t a = nullptr, b = nullptr;
-            if (timing_on(c, BK_K_ALLREDUCE)) {
-                CHK(get_event(c, &a));
-                CHK(get_event(c, &b));
-                HIPCHK(hipEventRecord(a, c->stream));
-            }
             RCCLCHK(ncclAllReduce(U, U, (size_t)usz, ncclDouble, ncclSum, c->comm, c->stream));
-            if (timing_on(c, BK_K_ALLREDUCE)) {
-                HIPCHK(hipEventRecord(b, c->stream));
-                c->pending.push_back({BK_K_ALLREDUCE, a, b});
-            }
         } else {
             CHK(ensure(c->Ug, (size_t)usz * c->nranks * sizeof(double)));
             double *Ug = (double *)c->Ug.p;
-            hipEvent_t a = nullptr, b = nullptr;
-            if (timing_on(c, BK_K_ALLREDUCE)) {
-                CHK(get_event(c, &a));
-                CHK(get_event(c, &b));
-                HIPCHK(hipEventRecord(a, c->stream));
-            }
             RCCLCHK(ncclAllGather(U, Ug, (size_t)usz, ncclDouble, c->comm, c->stream));
             HIPCHK(launch_sum_ranks(Ug, c->nranks, usz, U, c->stream));
-            if (timing_on(c, BK_K_ALLREDUCE)) {
-                HIPCHK(hipEventRecord(b, c->stream));
-                c->pending.push_back({BK_K_ALLREDUCE, a, b});
-            }
         }
+        if (timing_on(c, BK_K_ALLREDUCE)) {
+            HIPCHK(hipEventRecord(b, c->stream));
+            c->pending.push_back({BK_K_ALLREDUCE, a, b});
+        }
+        c->exchanged_bytes += (double)usz * sizeof(double) * (c->deterministic ? c->nranks : 1);
+        ++c->exchanges;
     }
-    return stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, d_mean);
+    return stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores,
+                        dl > 0 ? d_mean : nullptr);
 }
+}  // namespace
+
+int bk_multikrum_sharded_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl,
+                                int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
+                                double *d_mean) {
+    if (dl > 0) {
+        CHK(check_common(c, dX, dtype, n, dl, ld));
+    } else {
+        // d_local = 0 is legal (an empty trailing shard): dX, ld and d_mean are unused
+        if (!c) return fail(BK_EINVAL, "null context");
+        if (dl < 0) return fail(BK_EINVAL, "d_local=%lld < 0", (long long)dl);
+        if (dtype != BK_F64 && dtype != BK_F32) return fail(BK_EINVAL, "bad dtype %d", dtype);
+    }
+    CHK(bk_check_args(n, dl > 0 ? dl : 1, f));
+    if (!d_sel) return fail(BK_EINVAL, "null d_sel_idx");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    if (c->nranks > 1 && !c->comm) return fail(BK_ERCCL, "bk_comm_init not called");
+    auto once = [&] { return sharded_once(c, dX, dtype, n, dl, ld, f, d_sel, d_scores, d_mean); };
+    if (certified(c, dtype)) return run_certified(c, once);
+    return once();
+}
+
+int bk_comm_size(bk_ctx *c, int *nranks, int *rank) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    int nr = 1, rk = 0;
+    if (c->comm) {
+        RCCLCHK(ncclCommCount(c->comm, &nr));
+        RCCLCHK(ncclCommUserRank(c->comm, &rk));
+    }
+    if (nranks) *nranks = c->comm ? nr : 0;
+    if (rank) *rank = rk;
+    return BK_OK;
+}
+
+int bk_comm_stats(bk_ctx *c, int64_t *exchanges, double *bytes) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (exchanges) *exchanges = c->exchanges;
+    if (bytes) *bytes = c->exchanged_bytes;
+    return BK_OK;
+}
+
+int bk_selection_margin(bk_ctx *c, double *gap, double *err_bound, int *near_tie) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    double mg[8];
+    CHK(read_margin(c, mg));
+    if (gap) *gap = mg[0];
+    if (err_bound) *err_bound = mg[1];
+    if (near_tie) *near_tie = mg[2] != 0.0 ? 1 : 0;
+    return BK_OK;
+}
+
+int bk_selection_margin_record(bk_ctx *c, double *record) {
+    if (!c || !record) return fail(BK_EINVAL, "null context / record");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    double mg[8];
+    CHK(read_margin(c, mg));
+    memcpy(record, mg, sizeof mg);
+    return BK_OK;
+}
+
+int64_t bk_certified_reruns(bk_ctx *c) { return c ? c->certified_reruns : 0; }
 
 // ---- one process, G GPUs --------------------------------------------------
 }  // extern "C"
@@ -956,6 +1122,22 @@ void group_shard(int64_t d, int G, int r, int64_t *c0, int64_t *dl) {
     *c0 = a;
     *dl = b - a;
 }
+
+// Error returns of bk_group_multikrum: every device's copy stream may still be
+// reading the caller's X, and D2H copies may still be writing sel / scores /
+// mean_out, so all streams of all contexts are drained unless disarmed.
+struct GroupDrain {
+    bk_group *g;
+    bool armed = true;
+    ~GroupDrain() {
+        if (!armed) return;
+        for (bk_ctx *c : g->ctx) {
+            DeviceGuard dg(c->device);
+            if (c->copy) (void)hipStreamSynchronize(c->copy);
+            (void)hipStreamSynchronize(c->stream);
+        }
+    }
+};
 
 int group_free_host(bk_group *g) {
     if (g->hpart) (void)hipHostFree(g->hpart);
@@ -1067,6 +1249,7 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
     const int64_t m = n - f;
     const int64_t usz = bk_upper_elems(n);
     std::vector<Plan> pls((size_t)G);
+    GroupDrain drain{g};
     // 1. per device: its column shard crosses PCIe in column chunks on the
     //    device's copy stream, each chunk's partial Gram (K1 + K1b) overlapped
     //    with the next chunk's copy (stage_host_pipelined)
@@ -1183,6 +1366,7 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
         DeviceGuard dg(g->ctx[(size_t)r]->device);
         HIPCHK(hipStreamSynchronize(g->ctx[(size_t)r]->stream));
     }
+    drain.armed = false;
     if (m_out) *m_out = m;
     return BK_OK;
 }
@@ -1307,6 +1491,8 @@ int bk_aggregate(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
     if (m == 0) return BK_OK;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
+    // on an error return, queued copies may still read X / hidx / global
+    HostDrain drain{c};
     const size_t es = esize(dtype);
     const void *dX = X;
     int64_t dld = ld;
@@ -1342,6 +1528,7 @@ int bk_aggregate(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
                               c->stream);
     }));
     HIPCHK(hipStreamSynchronize(c->stream));
+    drain.armed = false;
     return BK_OK;
 }
 
@@ -1414,6 +1601,8 @@ int bk_roni_set_validation(bk_ctx *c, const double *Xv, int64_t nv, int64_t d, i
     if (!Xv || !yv) return fail(BK_EINVAL, "null Xv / yv");
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
+    c->roni_nv = 0;  // invalid until the new set has landed
+    HostDrain drain{c};
     CHK(ensure(c->roni_X, (size_t)nv * d * sizeof(double)));
     CHK(ensure(c->roni_y, (size_t)nv * sizeof(double)));
     HIPCHK(hipMemcpy2DAsync(c->roni_X.p, (size_t)d * sizeof(double), Xv, (size_t)ldv * sizeof(double),
@@ -1421,6 +1610,7 @@ int bk_roni_set_validation(bk_ctx *c, const double *Xv, int64_t nv, int64_t d, i
     HIPCHK(hipMemcpyAsync(c->roni_y.p, yv, (size_t)nv * sizeof(double), hipMemcpyHostToDevice,
                           c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    drain.armed = false;
     c->roni_nv = nv;
     c->roni_dim = d;
     return BK_OK;
@@ -1429,14 +1619,15 @@ int bk_roni_set_validation(bk_ctx *c, const double *Xv, int64_t nv, int64_t d, i
 int bk_roni(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_t d, int64_t ld,
             double *scores) {
     if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);  // roni_nv / roni_dim change under it
     if (c->roni_nv < 1) return fail(BK_EINVAL, "no validation set: call bk_roni_set_validation");
     if (d != c->roni_dim)
         return fail(BK_EINVAL, "d=%lld != validation set's %lld", (long long)d, (long long)c->roni_dim);
     CHK(check_roni(c->roni_nv, d, d, n, ld));
     if (!ww || (n > 0 && (!deltas || !scores))) return fail(BK_EINVAL, "null pointer argument");
     if (n == 0) return BK_OK;
-    std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
+    HostDrain drain{c};  // error returns: queued H2D copies may still read ww / deltas
     CHK(ensure(c->roni_w, (size_t)d * sizeof(double)));
     CHK(ensure(c->roni_d, (size_t)n * d * sizeof(double)));
     CHK(ensure(c->roni_s, (size_t)n * sizeof(double)));
@@ -1461,5 +1652,6 @@ int bk_roni(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_
                               c->stream);
     }));
     HIPCHK(hipStreamSynchronize(c->stream));
+    drain.armed = false;
     return BK_OK;
 }

@@ -87,10 +87,14 @@ hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, c
 hipError_t launch_reduce(const double *part, const Plan &pl, double *U, hipStream_t st);
 hipError_t launch_sum_ranks(const double *Ug, int R, int64_t stride, double *U, hipStream_t st);
 hipError_t launch_add_upper(double *U, const double *P, int64_t count, hipStream_t st);
-hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores,
+hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores, double *diag,
                          hipStream_t st);
-hipError_t launch_rank(const double *scores, int n, int m, int *mask, hipStream_t st);
-hipError_t launch_compact(const int *mask, int n, int64_t *sel, hipStream_t st);
+hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bnd,
+                       hipStream_t st);
+// margin: nullable (8 doubles, see k_compact); dcols: the packed upper's trailing element
+hipError_t launch_compact(const int *mask, int n, int64_t *sel, const double *diag,
+                          const double *bnd, const double *dcols, int64_t k, double u_gram,
+                          double *margin, hipStream_t st);
 hipError_t launch_mean(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel, int m,
                        double *mean, int num_cu, hipStream_t st);
 // global[c] += X[idx[0]][c] + X[idx[1]][c] + ... (sequential, idx order)

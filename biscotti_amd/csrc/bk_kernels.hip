@@ -870,7 +870,11 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64
 __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part,
                                                  const int *__restrict__ red,
                                                  const int *__restrict__ wglist,
-                                                 double *__restrict__ U) {
+                                                 double *__restrict__ U, int64_t usz,
+                                                 double dcols) {
+    // the packed upper's trailing element: the Gram's column count (summed
+    // with the tiles by every exchange, so it is the total d; K3b's margin)
+    if (blockIdx.x == 0 && threadIdx.x == 0) U[usz] = dcols;
 #ifndef BK_REDUCE_V1
     // 64 elements per block, 2 per lane (16-B loads), 8 slabs in flight per
     // sub-list; the same order of adds as below (bitwise the same U)
@@ -943,7 +947,8 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
 // grid: ntile*16 blocks of 256 threads (4 rows x 64 cols each)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_reduce(const double *__restrict__ part, int ntile, int S,
-                                                double *__restrict__ U) {
+                                                double *__restrict__ U, double dcols) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) U[(int64_t)ntile * 4096] = dcols;  // as k_reduce3
     const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
     const int e = chunk * 256 + threadIdx.x;
     const double *p = part + (int64_t)u * 4096 + e;
@@ -991,11 +996,13 @@ __device__ __forceinline__ double u_at(const double *__restrict__ U, int T, int 
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_scores(const double *__restrict__ U, int T_, int n,
-                                               int npow2, int64_t k, double *__restrict__ scores) {
+                                               int npow2, int64_t k, double *__restrict__ scores,
+                                               double *__restrict__ diag) {
     extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
     __shared__ double red[NT / 64];
     const int i = blockIdx.x, tid = threadIdx.x;
     const double di = u_at(U, T_, i, i);
+    if (tid == 0) diag[i] = di;  // ||x_i||^2 for the selection margin (K3b)
     for (int j = tid; j < npow2; j += NT) {
         uint64_t key = ~0ULL;  // padding sorts after every real value (NaN included)
         if (j < n) {
@@ -1039,12 +1046,16 @@ __global__ __launch_bounds__(NT) void k_scores(const double *__restrict__ U, int
 // ---------------------------------------------------------------------------
 // K3: rank_i = #{j : key_j < key_i} + #{j < i : key_j == key_i}; mask = rank < m
 // ---------------------------------------------------------------------------
-// one wave per row: lanes sweep j, a ballot counts the keys ranked before i
+// one wave per row: lanes sweep j, a ballot counts the keys ranked before i.
+// The ranks are a permutation of 0..n-1, so exactly one row writes each of
+// bnd[0] = the highest selected score (rank m-1) and bnd[1] = the lowest
+// rejected one (rank m): the selection boundary, for K3b's margin.
 __global__ __launch_bounds__(256) void k_rank(const double *__restrict__ scores, int n, int m,
-                                              int *__restrict__ mask) {
+                                              int *__restrict__ mask, double *__restrict__ bnd) {
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (i >= n) return;  // wave-uniform
-    const uint64_t ki = dkey(scores[i]);
+    const double si = scores[i];
+    const uint64_t ki = dkey(si);
     int cnt = 0;
     for (int j0 = 0; j0 < n; j0 += 64) {
         const int j = j0 + lane;
@@ -1055,13 +1066,40 @@ __global__ __launch_bounds__(256) void k_rank(const double *__restrict__ scores,
         }
         cnt += __popcll(__ballot(before));
     }
-    if (lane == 0) mask[i] = cnt < m ? 1 : 0;
+    if (lane == 0) {
+        mask[i] = cnt < m ? 1 : 0;
+        if (cnt == m - 1) bnd[0] = si;
+        if (cnt == m) bnd[1] = si;
+    }
 }
 
-// K3b: ascending compaction of mask (single workgroup of 1024 threads)
+// gamma_n = n u / (1 - n u) (Higham's bound for a length-n dot product or sum
+// in any order, every step one rounding); +inf once n u >= 1
+__device__ __forceinline__ double gamma_n(double nn, double u) {
+    const double t = nn * u;
+    return t < 1.0 ? t / (1.0 - t) : __builtin_inf();
+}
+
+// K3b: ascending compaction of mask (single workgroup of 1024 threads), then
+// the selection margin (SURVEY.md §7 "Hard parts", §8(d)):
+//   gap       = s[rank m] - s[rank m-1]  (lowest rejected - highest selected)
+//   err_bound = 2 (e_here + e_ref),  e = 4 k M' (gamma_{d+2}(u_G) + 2 u + gamma_k(u))
+// where M' = max finite G_ii (1 + 2 gamma_{d+2}(u_G)) bounds max ||x_i||^2, u =
+// 2^-53 (the distance and score arithmetic, and numpy's BLAS Gram), u_G the
+// Gram's unit roundoff here (2^-53; 2^-24 on the fp32 MFMA), d = the Gram's
+// column count (carried in the packed upper's trailing element, so it is the
+// TOTAL d after a multi-GPU exchange).  Every computed score lies within e of
+// the exact one, so whenever gap > err_bound the reference selects exactly this
+// set; otherwise near_tie = 1 (also for exact ties, e.g. k = 0).
+// margin[0..7] = {gap, err_bound, near_tie, M, s_lo, s_hi, d, k}
 __global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, int n,
-                                                  int64_t *__restrict__ sel) {
+                                                  int64_t *__restrict__ sel,
+                                                  const double *__restrict__ diag,
+                                                  const double *__restrict__ bnd,
+                                                  const double *__restrict__ dcols, int64_t k,
+                                                  double u_gram, double *__restrict__ margin) {
     __shared__ int pre[1024];
+    __shared__ double mx[16];
     const int tid = threadIdx.x;
     const int chunk = (n + 1023) / 1024;
     const int c0 = min(n, tid * chunk), c1 = min(n, c0 + chunk);
@@ -1078,6 +1116,40 @@ __global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, 
     int pos = pre[tid] - cnt;
     for (int j = c0; j < c1; ++j)
         if (mask[j]) sel[pos++] = j;
+    if (!margin) return;  // block-uniform
+    // M = max finite G_ii (NaN / Inf rows have NaN / Inf scores in the
+    // reference too: they order last, deterministically)
+    double m = 0.0;
+    for (int j = tid; j < n; j += 1024) {
+        const double v = diag[j];
+        if (v == v && v < __builtin_inf() && v > m) m = v;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+    if ((tid & 63) == 0) mx[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) {
+        double M = 0.0;
+        for (int w = 0; w < 16; ++w) M = fmax(M, mx[w]);
+        const double u = 0x1p-53, dg = *dcols, kk = (double)k;
+        const double gG = gamma_n(dg + 2.0, u_gram), gR = gamma_n(dg + 2.0, u);
+        const double gk = gamma_n(kk, u);
+        const double Mt = M * (1.0 + 2.0 * gG);
+        const double e_here = 4.0 * kk * Mt * (gG + 2.0 * u + gk);
+        const double e_ref = 4.0 * kk * Mt * (gR + 2.0 * u + gk);
+        const double bound = 2.0 * (e_here + e_ref) * (1.0 + 0x1p-40);
+        const double lo = bnd[0], hi = bnd[1];
+        // NaN scores rank last here and in numpy: a finite-to-NaN boundary is certain
+        const double gap = (hi != hi && lo == lo) ? __builtin_inf() : hi - lo;
+        margin[0] = gap;
+        margin[1] = bound;
+        margin[2] = (gap > bound) ? 0.0 : 1.0;  // NaN gap -> near tie
+        margin[3] = M;
+        margin[4] = lo;
+        margin[5] = hi;
+        margin[6] = dg;
+        margin[7] = kk;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1223,7 +1295,7 @@ hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, c
 
 hipError_t launch_reduce(const double *part, const Plan &pl, double *U, hipStream_t st) {
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)pl.ntile * 16), dim3(256), 0, st, part, pl.ntile,
-                       pl.S, U);
+                       pl.S, U, (double)pl.d);
     return hipGetLastError();
 }
 
@@ -1258,25 +1330,31 @@ static int next_pow2(int v) {
     return p;
 }
 
-hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores,
+hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores, double *diag,
                          hipStream_t st) {
     const int np2 = next_pow2(n < 2 ? 2 : n);
     const size_t lds = (size_t)np2 * sizeof(uint64_t);
     if (np2 <= 2048) {
-        hipLaunchKernelGGL(k_scores<256>, dim3(n), dim3(256), lds, st, U, T, n, np2, k, scores);
+        hipLaunchKernelGGL(k_scores<256>, dim3(n), dim3(256), lds, st, U, T, n, np2, k, scores,
+                           diag);
     } else {
-        hipLaunchKernelGGL(k_scores<1024>, dim3(n), dim3(1024), lds, st, U, T, n, np2, k, scores);
+        hipLaunchKernelGGL(k_scores<1024>, dim3(n), dim3(1024), lds, st, U, T, n, np2, k, scores,
+                           diag);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_rank(const double *scores, int n, int m, int *mask, hipStream_t st) {
-    hipLaunchKernelGGL(k_rank, dim3((n + 3) / 4), dim3(256), 0, st, scores, n, m, mask);
+hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bnd,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_rank, dim3((n + 3) / 4), dim3(256), 0, st, scores, n, m, mask, bnd);
     return hipGetLastError();
 }
 
-hipError_t launch_compact(const int *mask, int n, int64_t *sel, hipStream_t st) {
-    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, st, mask, n, sel);
+hipError_t launch_compact(const int *mask, int n, int64_t *sel, const double *diag,
+                          const double *bnd, const double *dcols, int64_t k, double u_gram,
+                          double *margin, hipStream_t st) {
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, st, mask, n, sel, diag, bnd, dcols, k,
+                       u_gram, margin);
     return hipGetLastError();
 }
 
@@ -1368,12 +1446,13 @@ hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, 
 }
 
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st) {
+    const int64_t usz = (int64_t)pl.ntile * 4096;
 #ifndef BK_REDUCE_V1
     hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 64), dim3(256), 0, st, part, pl.d_red,
-                       pl.d_wglist, U);
+                       pl.d_wglist, U, usz, (double)pl.d);
 #else
     hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 128), dim3(256), 0, st, part, pl.d_red,
-                       pl.d_wglist, U);
+                       pl.d_wglist, U, usz, (double)pl.d);
 #endif
     return hipGetLastError();
 }

@@ -34,13 +34,16 @@ def all_shards(d, world, align=ALIGN):
 
 
 def upper_elems(n):
+    """bk_upper_elems: the 64x64 upper sub-tiles + one trailing element, the
+    Gram's column count (summed by the exchange with the tiles)."""
     T = (n + 63) // 64
-    return T * (T + 1) // 2 * 4096
+    return T * (T + 1) // 2 * 4096 + 1
 
 
-def pack_upper(G):
+def pack_upper(G, d_cols=0):
     """Dense symmetric n x n -> the packed 64x64-sub-tile upper layout libbk
-    exchanges (bk_upper_elems(n) doubles, sub-tiles (bi <= bj) row-major)."""
+    exchanges (bk_upper_elems(n) doubles, sub-tiles (bi <= bj) row-major, then
+    the column count d_cols the partial was taken over)."""
     n = G.shape[0]
     T = (n + 63) // 64
     Gp = np.zeros((T * 64, T * 64))
@@ -51,13 +54,13 @@ def pack_upper(G):
         for bj in range(bi, T):
             out[u] = Gp[bi * 64:(bi + 1) * 64, bj * 64:(bj + 1) * 64]
             u += 1
-    return out.reshape(-1)
+    return np.concatenate([out.reshape(-1), [float(d_cols)]])
 
 
 def unpack_upper(U, n):
     """Inverse of pack_upper (upper sub-tiles; diagonal sub-tiles: i <= j used)."""
     T = (n + 63) // 64
-    tiles = np.asarray(U).reshape(-1, 64, 64)
+    tiles = np.asarray(U)[:T * (T + 1) // 2 * 4096].reshape(-1, 64, 64)
     Gp = np.zeros((T * 64, T * 64))
     u = 0
     for bi in range(T):

@@ -274,9 +274,37 @@ class Engine:
     def timing_enable(self, on=True):
         check(lib().bk_timing_enable(self._ctx, 1 if on else 0))
 
+    # ---- selection margin (bk_selection_margin): where the selection may
+    #      legitimately differ from numpy's (logistic_validator.py:45,59-63) --
+    def selection_margin(self):
+        """{gap, err_bound, near_tie, M, s_lo, s_hi, d, k} of the last call on
+        this context; near_tie False proves the reference selects the same set."""
+        rec = (ctypes.c_double * 8)()
+        check(lib().bk_selection_margin_record(self._ctx, rec))
+        keys = ("gap", "err_bound", "near_tie", "M", "s_lo", "s_hi", "d", "k")
+        out = dict(zip(keys, (float(x) for x in rec)))
+        out["near_tie"] = bool(out["near_tie"])
+        out["d"] = int(out["d"])
+        out["k"] = int(out["k"])
+        return out
+
+    def certified_reruns(self):
+        return int(lib().bk_certified_reruns(self._ctx))
+
+    def comm_size(self):
+        nr, rk = ctypes.c_int(0), ctypes.c_int(0)
+        check(lib().bk_comm_size(self._ctx, ctypes.byref(nr), ctypes.byref(rk)))
+        return nr.value, rk.value
+
+    def comm_stats(self):
+        ex, by = ctypes.c_int64(0), ctypes.c_double(0)
+        check(lib().bk_comm_stats(self._ctx, ctypes.byref(ex), ctypes.byref(by)))
+        return ex.value, by.value
+
     def set_f32_mode(self, mode):
-        """_lib.BK_F32_EXACT (fp32 rows widened onto the fp64 MFMA, default) or
-        _lib.BK_F32_MFMA (the fp32 MFMA, fp32 accumulation per K1 segment)."""
+        """_lib.BK_F32_EXACT (fp32 rows widened onto the fp64 MFMA, default),
+        _lib.BK_F32_MFMA (the fp32 MFMA, fp32 accumulation per K1 segment), or
+        _lib.BK_F32_CERTIFIED (the fp32 MFMA, re-run exactly on a near tie)."""
         check(lib().bk_set_f32_mode(self._ctx, int(mode)))
 
     def graph_enable(self, on=True):

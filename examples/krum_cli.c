@@ -4,11 +4,13 @@
  * i.e. of KRUMValidator.getTopKRUMIndex (DistSys/krum.go:100-166):
  *
  *   bk_create -> bk_check_args -> bk_stage_alloc (C-owned pinned staging) ->
- *   pack rows -> bk_multikrum(BK_HOST_PINNED) -> selected indices -> bk_destroy
+ *   pack rows -> bk_multikrum(BK_HOST_PINNED) -> selected indices ->
+ *   bk_selection_margin (near-tie log) -> bk_destroy
  *
  *   krum_cli <file> <n> <d> <f>     file: n*d little-endian float64, row-major
  *
- * Prints "m=<m>" and then the m selected indices (ascending), one per line;
+ * Prints "m=<m>" and then the m selected indices (ascending), one per line,
+ * and the selection margin on stderr;
  * on any error prints bk_last_error() and exits 1 (the shim rejects every
  * update in that case).  Built by __graft_entry__.build() with gcc.
  */
@@ -57,6 +59,14 @@ int main(int argc, char **argv)
     }
     printf("m=%lld\n", (long long)m);
     for (int64_t i = 0; i < m; ++i) printf("%lld\n", (long long)sel[i]);
+    /* the shim's near-tie log (bk_selection_margin): stderr, stdout stays the set */
+    double gap = 0, bound = 0;
+    int near = 0;
+    if (bk_selection_margin(ctx, &gap, &bound, &near) != BK_OK) {
+        fprintf(stderr, "krum_cli: bk_selection_margin: %s\n", bk_last_error());
+        goto out;
+    }
+    fprintf(stderr, "margin: gap=%.17g err_bound=%.17g near_tie=%d\n", gap, bound, near);
     rc = 0;
 out:
     if (fp) fclose(fp);

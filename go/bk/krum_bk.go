@@ -122,6 +122,7 @@ func (krumval *KRUMValidator) getTopKRUMIndex(deltas [][]float64) []int {
 		outLog.Printf("Krum failed (%d): %s", int(st), C.GoString(C.bk_last_error()))
 		return []int{}
 	}
+	logMargin()
 	out := make([]int, int(mOut))
 	for i := range out {
 		out[i] = int(sel[i])
@@ -192,11 +193,27 @@ func (krumval *KRUMValidator) getTopKRUMIndexNoised(updates []Update) []int {
 		outLog.Printf("Krum failed (%d): %s", int(st), C.GoString(C.bk_last_error()))
 		return []int{}
 	}
+	logMargin()
 	out := make([]int, int(mOut))
 	for i := range out {
 		out[i] = int(sel[i])
 	}
 	return out
+}
+
+// logMargin reports a selection the reference could legitimately make
+// differently (bk_selection_margin): the boundary gap between the highest
+// selected and the lowest rejected score is within the rounding bound of the
+// scores, or an exact tie (k = n-f-2 = 0 makes every score 0, as on the
+// localTest.sh n = 4 verifier).  Otherwise numpy's argpartition over its own
+// BLAS-rounded scores (logistic_validator.py:45,59-63) provably picks the same set.
+func logMargin() {
+	var gap, bound C.double
+	var near C.int
+	if C.bk_selection_margin(bkCtx, &gap, &bound, &near) == C.BK_OK && near != 0 {
+		outLog.Printf("Krum: near tie at the selection boundary (gap %g <= bound %g); "+
+			"ties resolved to the lower index", float64(gap), float64(bound))
+	}
 }
 
 func noisedDeltas(updates []Update) [][]float64 {

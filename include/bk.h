@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 6
+#define BK_ABI_VERSION 7
 
 typedef struct bk_ctx bk_ctx;
 
@@ -113,12 +113,44 @@ int bk_graph_enable(bk_ctx *ctx, int on);
  * config E: the selection matches wherever the score gap at the boundary
  * exceeds the fp32 Gram error bound (~2 k gamma_d max|x_i|^2).  The mean is
  * unchanged (fp64 accumulation of the fp32 rows).  No effect on fp64 rows. */
-enum bk_f32_mode { BK_F32_EXACT = 0, BK_F32_MFMA = 1 };
+enum bk_f32_mode { BK_F32_EXACT = 0, BK_F32_MFMA = 1, BK_F32_CERTIFIED = 2 };
+/* BK_F32_CERTIFIED: the fp32 MFMA, then -- only when the selection margin
+ * (bk_selection_margin) does not clear the fp32 bound -- the exact path on the
+ * same device-resident batch, whose outputs replace the first run's.  Never
+ * silently different from the reference where the exact path is not; the
+ * entries become synchronous (the decision reads the margin on the host).
+ * bk_group_multikrum runs such contexts as BK_F32_MFMA (check the margin). */
 int bk_set_f32_mode(bk_ctx *ctx, int mode);
+/* exact re-runs BK_F32_CERTIFIED has made on this context */
+int64_t bk_certified_reruns(bk_ctx *ctx);
+
+/* ---- selection margin: where the selection may legitimately differ from the
+ * reference's (SURVEY.md §7 "Hard parts", §8(d); logistic_validator.py:45,
+ * 59-63: argpartition over BLAS-rounded scores).  Every Multi-Krum call
+ * (any entry) leaves on its context, computed on the device by the finish:
+ *   gap       = s[rank m] - s[rank m-1], the lowest rejected score minus the
+ *               highest selected one (+inf across a finite -> NaN boundary)
+ *   err_bound = 2 (e_here + e_ref),  e = 4 k M' (gamma_{d+2}(u_G) + 2u + gamma_k(u))
+ *               with M' >= max_i ||x_i||^2 (finite rows), u = 2^-53, u_G the
+ *               Gram's unit roundoff here (2^-53, or 2^-24 on the fp32 MFMA),
+ *               gamma_j(u) = j u / (1 - j u), d the Gram's total column count
+ *               (after a multi-GPU exchange too), k = n - f - 2
+ *   near_tie  = !(gap > err_bound)
+ * Any fp64 computation of the reference formula in any summation order --
+ * numpy's BLAS included -- gives scores within e of the exact ones, so when
+ * near_tie = 0 the reference provably selects exactly sel_idx.  near_tie = 1
+ * means the boundary is within rounding (or an exact tie, e.g. k = 0 where every
+ * score is 0): the lower-index tie rule decided, and numpy's choice may differ.
+ * Reads the record of the last call (synchronizes the context stream). */
+int bk_selection_margin(bk_ctx *ctx, double *gap, double *err_bound, int *near_tie);
+/* the whole record: {gap, err_bound, near_tie, M, s_lo, s_hi, d, k} (8 doubles) */
+int bk_selection_margin_record(bk_ctx *ctx, double *record);
 
 /* ---- dimension-sharded stages (one process / device per column shard) ----
- * Packed upper-triangle Gram: bk_upper_elems(n) doubles.  Summing the packed
- * partials of all shards gives the Gram of the full batch. */
+ * Packed upper-triangle Gram: bk_upper_elems(n) doubles = the 64x64 upper
+ * sub-tiles, then one trailing element holding the column count.  Summing the
+ * packed partials of all shards (trailing elements included) gives the Gram of
+ * the full batch and its total d, which the selection margin uses. */
 int64_t bk_upper_elems(int64_t n);
 int bk_gram_upper_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
                          int64_t ld, double *d_upper);
@@ -137,9 +169,17 @@ int bk_comm_init(bk_ctx *ctx, int nranks, int rank, const void *id /* BK_UNIQUE_
 int bk_comm_set_mode(bk_ctx *ctx, int deterministic);
 /* Partial Gram of the local column shard -> all-reduce -> scores/selection
  * (redundant on every rank) -> mean of the local columns.  Async on stream. */
+/* d_local = 0 is allowed (an empty trailing shard: dX_local, ld and
+ * d_mean_local unused); the rank still joins the exchange. */
 int bk_multikrum_sharded_device(bk_ctx *ctx, const void *dX_local, int dtype, int64_t n,
                                 int64_t d_local, int64_t ld, int64_t f, int64_t *d_sel_idx,
                                 double *d_scores, double *d_mean_local);
+/* the communicator's size and this rank (ncclCommCount / ncclCommUserRank);
+ * nranks = 0 when bk_comm_init was not called */
+int bk_comm_size(bk_ctx *ctx, int *nranks, int *rank);
+/* exchanges of the packed Gram made on this context, and the bytes this rank
+ * put into them (all-reduce: bk_upper_elems(n) * 8 each; all-gather: x nranks) */
+int bk_comm_stats(bk_ctx *ctx, int64_t *exchanges, double *bytes);
 
 /* ---- one process, G GPUs: the Go verifier's form ------
  * A verifier is ONE process holding [][]float64 in host memory

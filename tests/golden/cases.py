@@ -40,6 +40,16 @@ CASES = {
     "n1000_d2000": dict(n=1000, d=2000, f=300, seed=SEED0 + 25, nbyz=250),
     "n2500_d512": dict(n=2500, d=512, f=700, seed=SEED0 + 26, nbyz=600),
     "n129_d4097": dict(n=129, d=4097, f=40, seed=SEED0 + 27, nbyz=40),
+    # --- the selection boundary INSIDE the honest cluster (nbyz < f): honest
+    #     rows are rejected too, and the boundary gap is a tiny fraction of the
+    #     scores (the A-E goldens separate a 50-sigma Byzantine
+    #     cluster, which any Gram within ~1e-3 would select identically) ---------
+    "B_tight": dict(n=100, d=7850, f=30, seed=SEED0 + 31, nbyz=10, flags=FP32ROUND),
+    "C_tight": dict(n=1024, d=131072, f=307, seed=SEED0 + 32, nbyz=200, large=True),
+    "E_tight_fp32": dict(n=4096, d=262144, f=1228, seed=SEED0 + 33, nbyz=800, dtype="float32",
+                         large=True),
+    "fp32_tight_700x65536": dict(n=700, d=65536, f=210, seed=SEED0 + 34, nbyz=100,
+                                 dtype="float32", large=True),
 }
 
 MEAN_FULL_MAX_D = 8192   # store the full mean up to this d; sampled coords above

@@ -41,7 +41,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_names():
     L = _lib.lib()
-    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 6
+    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 7
     assert L.bk_kernel_name(0) == b"k_gram"
     assert L.bk_kernel_name(99) == b"?"
     assert len(_lib.KERNELS) == 15
@@ -59,11 +59,15 @@ def test_check_args(n, d, f, status):
 
 
 def test_upper_elems():
+    """64x64 upper sub-tiles + the trailing column-count element."""
+    from biscotti_amd import dist as D
     L = _lib.lib()
-    assert L.bk_upper_elems(1) == 4096
-    assert L.bk_upper_elems(64) == 4096
-    assert L.bk_upper_elems(65) == 3 * 4096
-    assert L.bk_upper_elems(512) == 36 * 4096
+    assert L.bk_upper_elems(1) == 4096 + 1
+    assert L.bk_upper_elems(64) == 4096 + 1
+    assert L.bk_upper_elems(65) == 3 * 4096 + 1
+    assert L.bk_upper_elems(512) == 36 * 4096 + 1
+    for n in (1, 63, 64, 65, 512, 4097):
+        assert D.upper_elems(n) == L.bk_upper_elems(n)
 
 
 def test_plan_fills_the_chip():
@@ -114,6 +118,14 @@ def test_null_and_bad_arguments_do_not_crash():
     assert L.bk_set_f32_mode(None, _lib.BK_F32_MFMA) == _lib.BK_EINVAL
     assert L.bk_multikrum_noised(None, None, 10, None, 1, 10, _lib.BK_HOST, 10, 10, 2, None, None,
                                  None, None, None, 10) == _lib.BK_EINVAL
+    assert L.bk_set_f32_mode(None, _lib.BK_F32_CERTIFIED) == _lib.BK_EINVAL
+    assert L.bk_selection_margin(None, None, None, None) == _lib.BK_EINVAL
+    assert L.bk_selection_margin_record(None, None) == _lib.BK_EINVAL
+    assert L.bk_certified_reruns(None) == 0
+    assert L.bk_comm_size(None, None, None) == _lib.BK_EINVAL
+    assert L.bk_comm_stats(None, None, None) == _lib.BK_EINVAL
+    assert L.bk_multikrum_sharded_device(None, None, 0, 10, 0, 0, 2, None, None,
+                                         None) == _lib.BK_EINVAL
 
 
 def test_no_gpu_fails_loudly():

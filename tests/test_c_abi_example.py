@@ -42,3 +42,4 @@ def test_c_caller_matches_oracle(cli, oracle, tmp_path, n, d, f):
     assert lines[0] == "m=%d" % (n - f)
     sel = np.array([int(x) for x in lines[1:]], dtype=np.int64)
     assert np.array_equal(sel, oracle.krum(X, f)[0])
+    assert "near_tie=0" in r.stderr, r.stderr  # separated synthetic batches: certified

@@ -40,7 +40,7 @@ def _worker(rank, world, port, names, q):
 
     class OracleSharded(D.ShardedKrum):
         def gram_partial(self, Xl):
-            return D.pack_upper(O.gram(Xl))
+            return D.pack_upper(O.gram(Xl), Xl.shape[1])
 
         def exchange(self, U):
             t = torch.from_numpy(U.copy())

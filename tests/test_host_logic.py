@@ -33,10 +33,11 @@ def test_pack_unpack_roundtrip():
 
 def test_packed_partials_sum_to_full_gram(oracle):
     X = oracle.synth(70, 1000, 11, 10)
-    full = D.pack_upper(oracle.gram(X))
-    parts = sum(D.pack_upper(oracle.gram(np.ascontiguousarray(X[:, c0:c0 + dl])))
+    full = D.pack_upper(oracle.gram(X), 1000)
+    parts = sum(D.pack_upper(oracle.gram(np.ascontiguousarray(X[:, c0:c0 + dl])), dl)
                 for c0, dl in D.all_shards(1000, 3))
     assert np.allclose(parts, full, rtol=1e-12, atol=1e-15)
+    assert parts[-1] == 1000.0  # the trailing element sums to the total column count
 
 
 def test_validator_bookkeeping_mirrors_krum_go():
