@@ -84,13 +84,22 @@ def test_config_E_golden(f32eng, name):
                                 sc.data_ptr(), mean.data_ptr())
     f32eng.synchronize()
     g = GU.load(name)
-    assert np.array_equal(sel.cpu().numpy(), g["sel"])
+    # the separated config-E golden selects identically; the tight ones (boundary
+    # inside the honest cluster) may differ, but only with the near-tie flag
+    # raised (tests/test_gpu_margin.py checks the record itself)
+    same = np.array_equal(sel.cpu().numpy(), g["sel"])
+    if not same:
+        mg = f32eng.selection_margin()
+        assert mg["near_tie"] and not mg["gap"] > mg["err_bound"], mg
+    if name == "E_4096x262144_fp32":
+        assert np.array_equal(sel.cpu().numpy(), g["sel"])
     k = n - f - 2
     bound = 2 * k * (d * 2.0 ** -24) * float(np.max(g["sq"]))
     err = float(np.max(np.abs(sc.cpu().numpy() - g["scores"])))
     print("config E fp32 MFMA: max score error %.3e (bound %.3e, max score %.3e)"
           % (err, bound, float(np.max(g["scores"]))))
     assert err <= bound
-    GU.check_mean(mean.cpu().numpy(), g, GU.manifest()[name])
+    if same:  # a different (flagged) set has a different mean
+        GU.check_mean(mean.cpu().numpy(), g, GU.manifest()[name])
     del X
     torch.cuda.empty_cache()
