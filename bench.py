@@ -47,6 +47,54 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo; what lscpu prints)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def lib_sha16():
+    import hashlib
+    from biscotti_amd import _lib
+    return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
+
+
+def single_call(step, eng, barrier, world, dev, calls=7, idle_s=0.2):
+    """What one verifier call sees (krum.go:100-166 runs one Multi-Krum per
+    batch): each call starts after >= 150 ms of GPU idle, so the shader clock
+    has dropped (DVFS) and the step pays the ramp.  Median over `calls` of the
+    whole step (max over ranks) and of K1 (HIP events on libbk's stream)."""
+    import torch
+    import torch.distributed as tdist
+    eng.timing_select(["k_gram"])
+    steps_ms, k1_ms = [], []
+    prev = 0.0
+    for _ in range(calls):
+        torch.cuda.synchronize()
+        barrier()
+        time.sleep(idle_s)
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) * 1e3
+        if world > 1:
+            tt = torch.tensor([t], dtype=torch.float64, device=dev)
+            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+            t = float(tt.item())
+        steps_ms.append(t)
+        tot = eng.timing_read().get("k_gram", {"total_ms": prev})["total_ms"]
+        k1_ms.append(tot - prev)
+        prev = tot
+    eng.timing_select([])
+    return float(np.median(steps_ms)), float(np.median(k1_ms)), steps_ms
+
+
 def cpu_baseline(w, target_s=10.0, target_1core_s=6.0):
     """Time the oracle (C/OpenMP restatement of the reference's numpy krum,
     oracle/krum_oracle.c) on a bounded column sample of the same batch, on all
@@ -75,7 +123,7 @@ def cpu_baseline(w, target_s=10.0, target_1core_s=6.0):
     cores = O.num_threads()
     ds, t = sized(min(d, 32768), target_s)
     out = {"value": round(n * ds * es / t / 1e9, 4), "unit": "GB/s", "cores": cores,
-           "kind": "port",
+           "cpu_model": cpu_model(), "kind": "port",
            "sample": "oracle/krum_oracle.c (OpenMP, %d threads) full Multi-Krum (Gram, sort, "
                      "select, mean) on the first %d of %d columns of the same %dx%d batch, %.2f s"
                      % (cores, ds, d, n, d, t)}
@@ -378,6 +426,9 @@ def main():
     torch.cuda.synchronize()
     kbreak = eng.timing_read()
     eng.timing_enable(False)
+    # the selection margin of this batch (bk_selection_margin): near_tie False
+    # proves the reference's argpartition selects exactly this set
+    mg = eng.selection_margin()
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -468,15 +519,23 @@ def main():
     flops = n * (n + 1) * dl
     achieved = flops / (g["avg_ms"] * 1e-3) / 1e12
     peak = PEAK_TFLOPS["f64"]  # fp32 inputs are widened onto the fp64 MFMA path
-    traffic = None
+    # traffic: HBM bytes per K1 launch from the rocprofv3 PMC passes
+    # (tools/profile.sh -> tools/pmc_summary.py), used only when that record was
+    # taken with this very libbk.so build (sha256 prefix); otherwise null
+    traffic, traffic_src = None, None
     pmc_path = os.path.join(REPO, "profiles", "pmc_%s.json" % a.workload)
-    if os.path.exists(pmc_path) and world == 1:
+    if os.path.exists(pmc_path) and world == 1 and not emu:
         try:
-            traffic = json.load(open(pmc_path)).get("k_gram", {}).get("hbm_bytes_per_launch")
+            rec = json.load(open(pmc_path))
+            if rec.get("libbk_sha16") == lib_sha16():
+                traffic = rec.get("k_gram", {}).get("hbm_bytes_per_launch")
+                traffic_src = "profiles/pmc_%s.json (PMC passes of this libbk.so build)" % a.workload
+            else:
+                traffic_src = "stale: profiles/pmc_%s.json is from another libbk.so build" % a.workload
         except Exception:
             traffic = None
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
             "kernel": "k_gram", "kernel_avg_ms": round(g["avg_ms"], 4),
             "flops_per_launch": flops}
 
@@ -518,6 +577,42 @@ def main():
     }
     if variants:
         out["variants"] = variants
+
+    if parity is not None and not emu:
+        parity["margin"] = {"near_tie": mg["near_tie"], "gap": mg["gap"],
+                            "err_bound": mg["err_bound"]}
+
+    # one verifier call after idle (the DVFS ramp), beside the steady state
+    sc_step, sc_k1, sc_all = single_call(step, eng, barrier, world, dev)
+    sc_gbs = n * (dl if emu else d) * es / (sc_step * 1e-3) / 1e9
+    out["single_call"] = {
+        "what": "median of 7 calls, each after 200 ms of GPU idle (one Multi-Krum per batch, "
+                "krum.go:100-166): the clock ramp a verifier sees",
+        "ms": round(sc_step, 4), "GB_per_s": round(sc_gbs, 3),
+        "k_gram_ms": round(sc_k1, 4),
+        "k_gram_frac": round(flops / (sc_k1 * 1e-3) / 1e12 / peak, 4),
+        "step_roofline_frac": round(max(t_mfma, t_hbm) / sc_step, 4),
+        "calls_ms": [round(x, 4) for x in sc_all]}
+
+    if sharded:
+        # evidence that RCCL reached N ranks and that every rank selected the same set
+        import hashlib
+        nr, rk = eng.comm_size()
+        ex, by = eng.comm_stats()
+        h = hashlib.sha256(sel.cpu().numpy().tobytes()).hexdigest()[:16]
+        hs = [h]
+        if world > 1:
+            hs = [None] * world
+            tdist.all_gather_object(hs, h)
+        ar = kbreak.get("allreduce")
+        usz = int(_lib.lib().bk_upper_elems(n))
+        out["rccl"] = {
+            "nranks": nr, "rank": rk,
+            "mode": "all-gather + fixed-order sum" if a.deterministic else "all-reduce (sum)",
+            "bytes_per_exchange": usz * 8 * (nr if a.deterministic else 1),
+            "exchange_ms_avg": round(ar["avg_ms"], 4) if ar else None,
+            "exchanges_this_rank": ex, "bytes_this_rank": by,
+            "selected_set_sha16": h, "ranks_agree": len(set(hs)) == 1}
 
     if rank == 0 and world == 1 and not emu and not a.no_next_rows and w["dtype"] == "f64":
         out["next_rows"] = next_rows(eng, X, n, d, sel, m)

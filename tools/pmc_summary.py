@@ -28,15 +28,39 @@ def short(name):
     return s.split("(")[0].replace("bk::", "")
 
 
+def pass_durations(d):
+    """{dispatch id: duration ms} from the PMC pass's own kernel trace
+    (profile.sh runs every --pmc pass with --kernel-trace, never other domains)."""
+    p = os.path.join(d, "run_kernel_trace.csv")
+    out = {}
+    if os.path.exists(p):
+        for r in csv.DictReader(open(p)):
+            out[r.get("Dispatch_Id")] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    return out
+
+
 def load_pmc(d):
+    """Per kernel: mean of every counter over its dispatches, plus the physical
+    shader clock per dispatch, GRBM_GUI_ACTIVE / 8 XCDs / that dispatch's own
+    duration in the same pass (MI355X_MICROARCH.md, DVFS give-back)."""
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    clocks = collections.defaultdict(list)
     for sub in sorted(os.listdir(d)):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not sub.startswith("pmc") or not os.path.exists(p):
             continue
+        dur = pass_durations(os.path.join(d, sub))
         for r in csv.DictReader(open(p)):
-            agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
+            k = short(r["Kernel_Name"])
+            agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            t = dur.get(r.get("Dispatch_Id"))
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and t:
+                clocks[k].append(float(r["Counter_Value"]) / 8.0 / (t * 1e-3) / 1e9)
+    res = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
+    for k, v in clocks.items():
+        v = sorted(v)
+        res[k]["_clock_ghz_median"] = v[len(v) // 2]
+    return res
 
 
 def main():
@@ -66,8 +90,9 @@ def main():
         hr = 100.0 * hit / (hit + miss) if hit + miss else float("nan")
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
         gui = c.get("GRBM_GUI_ACTIVE", 0.0)
-        avg = res.get(k, {}).get("avg_ms_rocprof")
-        clk = (gui / 8.0) / (avg * 1e-3) / 1e9 if gui and avg else float("nan")
+        # the clock from each dispatch's own duration in the PMC pass; the
+        # all-call rocprof average mixes shapes (r1 reported an impossible 6.26 GHz)
+        clk = c.get("_clock_ghz_median", float("nan"))
         simd_cycles = gui / 8.0 * 1024 if gui else 0
         mb = 100.0 * busy / simd_cycles if simd_cycles else float("nan")
         res.setdefault(k, {}).update(fetch_kib=c["FETCH_SIZE"], read_bytes_corrected=rd,
@@ -94,13 +119,18 @@ def main():
                 lines += ["", "%s per dispatch (ms): %s" % (k1, " ".join("%.3f" % x for x in durs)),
                           "timed window (dispatches %d..%d, = bench.py's timed steps): avg %.3f ms"
                           % (w + 1, w + st, sum(win) / len(win))]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import hashlib
+    sha = hashlib.sha256(open(os.path.join(repo, "biscotti_amd", "libbk.so"), "rb").read()).hexdigest()[:16]
+    out_json["libbk_sha16"] = sha
     json.dump(out_json, open(out + ".json", "w"), indent=1)
     if k1 and "hbm_bytes_per_launch" in res[k1]:
-        # the file bench.py reads its roofline "traffic" from
-        pj = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                          "pmc_%s.json" % workload)
+        # the file bench.py reads its roofline "traffic" from (only while the
+        # library hash matches: bench.py checks libbk_sha16)
+        pj = os.path.join(repo, "profiles", "pmc_%s.json" % workload)
         json.dump({"workload": workload, "source": "%s.json (tools/profile.sh %s)"
-                   % (os.path.relpath(out, os.path.dirname(pj) + "/.."), os.path.basename(prof)),
+                   % (os.path.relpath(out, repo), os.path.basename(prof)),
+                   "libbk_sha16": sha,
                    "k_gram": {k: v for k, v in res[k1].items() if k != "dispatch_ms"}},
                   open(pj, "w"), indent=1)
     open(out + ".md", "w").write("\n".join(lines) + "\n")
