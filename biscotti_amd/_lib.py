@@ -18,7 +18,7 @@ BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
 BK_ABI_VERSION = 7
 BK_F32_EXACT, BK_F32_MFMA, BK_F32_CERTIFIED = 0, 1, 2
-KERNELS = ["k_gram", "k_reduce", "k_expand", "k_scores", "k_rank", "k_compact", "k_mean",
+KERNELS = ["k_gram", "k_reduce", "k_transpose", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni"]
 K = {name: i for i, name in enumerate(KERNELS)}
 

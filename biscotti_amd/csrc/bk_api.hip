@@ -56,7 +56,7 @@ int fail(int code, const char *fmt, ...) {
         if (_s != BK_OK) return _s; \
     } while (0)
 
-const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_expand", "k_scores",
+const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_transpose", "k_scores",
                                             "k_rank",    "k_compact", "k_mean",   "allreduce",
                                             "k_synth",   "h2d",       "d2h",
                                             "k_aggregate", "k_qsum",  "k_noise",
@@ -80,6 +80,7 @@ struct bk_ctx {
     DevBuf part, U, Ug, scores, mask, sel, X, mean, perm, trace, idx;
     // the selection margin of the last finish (K2 diag, K3 boundary scores, K3b record)
     DevBuf diag, bnd, margin;
+    DevBuf Ut;  // K2 at large n: transposed off-diagonal tiles + diagonal (k_transpose)
     int margin_valid = 0;
     // BK_F32_CERTIFIED: 1 while the exact re-run of a near-tie call is in progress
     int force_exact = 0;
@@ -172,7 +173,7 @@ void bind_epoch(bk_ctx *c) {
     DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,   &c->scores, &c->mask,   &c->sel,
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                      &c->noise, &c->diag, &c->bnd, &c->margin};
+                      &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -394,8 +395,20 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     // unit roundoff of this Gram's accumulation (the margin's bound)
     const double u_gram = f32_mfma_now(c, dtype) ? 0x1p-24 : 0x1p-53;
     const double *dcols = U + (size_t)pl.ntile * 4096;  // the packed upper's trailing element
+    const double *Ut = nullptr, *dg = nullptr;
+    if (scores_transposed((int)n)) {
+        // large n: transposed off-diagonal tiles + contiguous diagonal, so K2
+        // reads rows in 512-B runs (the packed upper's lower half is strided)
+        const size_t tiles = (size_t)pl.ntile * 4096;
+        CHK(ensure(c->Ut, (tiles + (size_t)pl.T * 64) * sizeof(double)));
+        double *ut = (double *)c->Ut.p;
+        CHK(timed(c, BK_K_EXPAND,
+                  [&] { return launch_transpose(U, pl.T, ut, ut + tiles, c->stream); }));
+        Ut = ut;
+        dg = ut + tiles;
+    }
     CHK(timed(c, BK_K_SCORES,
-              [&] { return launch_scores(U, pl.T, (int)n, k, sc, diag, c->stream); }));
+              [&] { return launch_scores(U, Ut, dg, pl.T, (int)n, k, sc, diag, c->stream); }));
     CHK(timed(c, BK_K_RANK,
               [&] { return launch_rank(sc, (int)n, (int)m, mask, bnd, c->stream); }));
     CHK(timed(c, BK_K_COMPACT, [&] {
@@ -670,7 +683,7 @@ void bk_destroy(bk_ctx *c) {
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->scores,
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                          &c->noise, &c->diag, &c->bnd, &c->margin};
+                          &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut};
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);

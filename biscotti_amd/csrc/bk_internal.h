@@ -87,8 +87,12 @@ hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, c
 hipError_t launch_reduce(const double *part, const Plan &pl, double *U, hipStream_t st);
 hipError_t launch_sum_ranks(const double *Ug, int R, int64_t stride, double *U, hipStream_t st);
 hipError_t launch_add_upper(double *U, const double *P, int64_t count, hipStream_t st);
-hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores, double *diag,
-                         hipStream_t st);
+// Ut / dg: nullable (large n: k_transpose's transposed off-diagonal tiles and
+// contiguous diagonal, for coalesced row reads)
+hipError_t launch_scores(const double *U, const double *Ut, const double *dg, int T, int n,
+                         int64_t k, double *scores, double *diag, hipStream_t st);
+bool scores_transposed(int n);
+hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipStream_t st);
 hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bnd,
                        hipStream_t st);
 // margin: nullable (8 doubles, see k_compact); dcols: the packed upper's trailing element

@@ -17,6 +17,8 @@
 // numpy reference evaluates it.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 #include <type_traits>
 
 #include "bk_internal.h"
@@ -1043,6 +1045,281 @@ __global__ __launch_bounds__(NT) void k_scores(const double *__restrict__ U, int
     }
 }
 
+// K2 v2: the same scores, bitwise, with the row's keys in REGISTERS.  Thread
+// t holds keys t*KPT .. t*KPT+KPT-1 (blocked).  Bitonic stages with a stride
+// below KPT are compare-exchanges inside a thread; strides up to the wave's
+// span (64 KPT keys) exchange across lanes -- DPP quad permutes for lane xor
+// 1 / 2, ds_swizzle (bit-mask mode, no LDS banks) for 4 / 8 / 16, ds_bpermute
+// for 32 -- with no barriers; only strides beyond a wave go through LDS.
+// Keys are the distances as fp64 (-0 -> +0), ordered by v_min/v_max_f64 (two
+// instructions per compare-exchange); a row holding a NaN (rare: NaN / Inf
+// updates) is sorted as v1's order-preserving u64 keys instead (NaN last).
+// The sorted row is written to LDS once and summed in v1's exact shape: v1's
+// NT_SUM threads (256, or 1024 above 2048 keys), each summing ranks 1+t,
+// 1+t+NT_SUM, ..., the wave butterfly, then the waves in order -- emulated
+// with H = NT_SUM / NT accumulators per thread.  Any correct sort of the same
+// keys gives the same array, so the scores are bitwise v1's.
+// Row loads: from the packed upper tiles (u_at), or -- for large n, after
+// k_transpose -- from Ut (the off-diagonal tiles transposed) and a contiguous
+// diagonal, so a row is read in 512-B runs instead of 8-B strided elements.
+template <typename K>
+struct K2Ord;
+template <>
+struct K2Ord<uint64_t> {
+    static __device__ __forceinline__ uint64_t lo(uint64_t a, uint64_t b) { return a < b ? a : b; }
+    static __device__ __forceinline__ uint64_t hi(uint64_t a, uint64_t b) { return a < b ? b : a; }
+    static __device__ __forceinline__ uint64_t bits(uint64_t a) { return a; }
+    static __device__ __forceinline__ uint64_t from(uint64_t b) { return b; }
+    static __device__ __forceinline__ double val(uint64_t a) { return dkey_inv(a); }
+};
+template <>
+struct K2Ord<double> {  // no NaN in the row: IEEE min / max
+    static __device__ __forceinline__ double lo(double a, double b) { return __builtin_fmin(a, b); }
+    static __device__ __forceinline__ double hi(double a, double b) { return __builtin_fmax(a, b); }
+    static __device__ __forceinline__ uint64_t bits(double a) { return (uint64_t)__double_as_longlong(a); }
+    static __device__ __forceinline__ double from(uint64_t b) { return __longlong_as_double((long long)b); }
+    static __device__ __forceinline__ double val(double a) { return a; }
+};
+
+template <typename K>
+__device__ __forceinline__ void k2_cas(K &a, K &b) {  // ascending: a gets the min
+    const K l = K2Ord<K>::lo(a, b), h = K2Ord<K>::hi(a, b);
+    a = l;
+    b = h;
+}
+
+// the 64-bit value of lane (lane ^ M), 0 < M <= 63
+template <int M>
+__device__ __forceinline__ uint64_t k2_xchg(uint64_t v) {
+    const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+    int a, b;
+    if constexpr (M <= 3) {  // DPP quad_perm: lane ^ M within each quad
+        constexpr int P = (0 ^ M) | ((1 ^ M) << 2) | ((2 ^ M) << 4) | ((3 ^ M) << 6);
+        a = __builtin_amdgcn_mov_dpp(lo, P, 0xF, 0xF, false);
+        b = __builtin_amdgcn_mov_dpp(hi, P, 0xF, 0xF, false);
+    } else if constexpr (M <= 31) {  // ds_swizzle bit-mask mode: and 0x1F, xor M
+        a = __builtin_amdgcn_ds_swizzle(lo, 0x1F | (M << 10));
+        b = __builtin_amdgcn_ds_swizzle(hi, 0x1F | (M << 10));
+    } else {
+        a = __shfl_xor(lo, M);
+        b = __shfl_xor(hi, M);
+    }
+    return (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32);
+}
+
+// a stage whose partner is lane ^ M, register q ^ XL (XL = 0: xor stage;
+// XL = KPT - 1: the mirror stage opening a merge); `lower`: this lane holds
+// the lower index of every pair, so it keeps the minima
+template <typename K, int KPT, int M, int XL>
+__device__ __forceinline__ void k2_lane_stage(K (&v)[KPT], bool lower) {
+    K o[KPT];
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) o[q] = K2Ord<K>::from(k2_xchg<M>(K2Ord<K>::bits(v[q])));
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+        const K w = o[q ^ XL];
+        const K l = K2Ord<K>::lo(v[q], w), h = K2Ord<K>::hi(v[q], w);
+        v[q] = lower ? l : h;
+    }
+}
+
+template <typename K, int KPT, int XL>
+__device__ __forceinline__ void k2_lane_dispatch(K (&v)[KPT], int m, bool lower) {
+    switch (m) {
+    case 1: k2_lane_stage<K, KPT, 1, XL>(v, lower); break;
+    case 2: k2_lane_stage<K, KPT, 2, XL>(v, lower); break;
+    case 3: k2_lane_stage<K, KPT, 3, XL>(v, lower); break;
+    case 4: k2_lane_stage<K, KPT, 4, XL>(v, lower); break;
+    case 7: k2_lane_stage<K, KPT, 7, XL>(v, lower); break;
+    case 8: k2_lane_stage<K, KPT, 8, XL>(v, lower); break;
+    case 15: k2_lane_stage<K, KPT, 15, XL>(v, lower); break;
+    case 16: k2_lane_stage<K, KPT, 16, XL>(v, lower); break;
+    case 31: k2_lane_stage<K, KPT, 31, XL>(v, lower); break;
+    case 32: k2_lane_stage<K, KPT, 32, XL>(v, lower); break;
+    default: k2_lane_stage<K, KPT, 63, XL>(v, lower); break;
+    }
+}
+
+// bitonic sort of N = NT * KPT keys, blocked (thread t holds keys t KPT ..),
+// in the all-ascending form: each merge of size s opens with the mirror stage
+// (partner e ^ (s - 1)) and continues with xor stages (e ^ s/4, ..., e ^ 1);
+// the lower index of every pair takes the minimum, so no stage needs a
+// direction.  The sorted keys end in keys_lds.
+template <typename K, int NT, int KPT>
+__device__ __forceinline__ void k2_sort(K (&v)[KPT], K *keys_lds, int N, int tid) {
+    constexpr int LK = KPT == 1 ? 0 : KPT == 2 ? 1 : KPT == 4 ? 2 : KPT == 8 ? 3 : 4;
+    constexpr int WSPAN = 64 * KPT;  // keys per wave
+    const int lane = tid & 63, e0 = tid * KPT;
+    for (int size = 2; size <= N; size <<= 1) {
+        // (1) the mirror stage
+        if (size <= KPT) {
+#pragma unroll
+            for (int q = 0; q < KPT; ++q) {
+                const int p = q ^ (size - 1);
+                if (q < p && ((q ^ p) & (size >> 1))) k2_cas(v[q], v[p]);
+            }
+        } else if (size <= WSPAN) {
+            const int m = (size - 1) >> LK;
+            k2_lane_dispatch<K, KPT, KPT - 1>(v, m, (lane & ((size >> 1) >> LK)) == 0);
+        } else {
+            __syncthreads();  // earlier readers of keys_lds are done
+#pragma unroll
+            for (int q = 0; q < KPT; ++q) keys_lds[e0 + q] = v[q];
+            __syncthreads();
+            const int half = size >> 1;
+            for (int p = tid; p < (N >> 1); p += NT) {
+                const int lo = (p / half) * size + (p & (half - 1));
+                const int hi = lo ^ (size - 1);
+                K a = keys_lds[lo], b = keys_lds[hi];
+                k2_cas(a, b);
+                keys_lds[lo] = a;
+                keys_lds[hi] = b;
+            }
+            __syncthreads();
+            // (2a) xor stages beyond the wave, still in LDS
+            int stride = size >> 2;
+            for (; stride >= WSPAN; stride >>= 1) {
+                for (int p = tid; p < (N >> 1); p += NT) {
+                    const int lo = 2 * p - (p & (stride - 1));
+                    const int hi = lo + stride;
+                    K a = keys_lds[lo], b = keys_lds[hi];
+                    k2_cas(a, b);
+                    keys_lds[lo] = a;
+                    keys_lds[hi] = b;
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int q = 0; q < KPT; ++q) v[q] = keys_lds[e0 + q];
+        }
+        // (2b) xor stages across lanes, then (2c) inside the thread
+        for (int stride = min(size >> 2, WSPAN >> 1); stride >= KPT; stride >>= 1) {
+            const int m = stride >> LK;
+            k2_lane_dispatch<K, KPT, 0>(v, m, (lane & m) == 0);
+        }
+#pragma unroll
+        for (int st = KPT / 2; st >= 1; st >>= 1) {
+            if (st > (size >> 2)) continue;
+#pragma unroll
+            for (int q = 0; q < KPT; ++q)
+                if ((q & st) == 0) k2_cas(v[q], v[q + st]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) keys_lds[e0 + q] = v[q];
+    __syncthreads();
+}
+
+// v1's summation shape over the sorted keys (virtual thread t' = tid + NT h)
+template <typename K, int NT, int NT_SUM>
+__device__ __forceinline__ double k2_sum(const K *keys_lds, int64_t k, int tid, double *red) {
+    constexpr int H = NT_SUM / NT;
+    const int lane = tid & 63;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+        double acc = 0.0;
+        for (int64_t r = 1 + tid + NT * h; r <= k; r += NT_SUM) acc += K2Ord<K>::val(keys_lds[r]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0) red[(tid >> 6) + (NT / 64) * h] = acc;
+    }
+    __syncthreads();
+    double sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT_SUM / 64; ++w) sum += red[w];
+    return sum;
+}
+
+// row i of G, element e: packed upper tiles, or (TR) Ut + contiguous diagonal
+template <bool TR>
+__device__ __forceinline__ double k2_g(const double *__restrict__ U, const double *__restrict__ Ut,
+                                       int T_, int i, int e) {
+    if constexpr (!TR) {
+        return u_at(U, T_, i, e);
+    } else {
+        const int br = i >> 6, bc = e >> 6, ir = i & 63, ic = e & 63;
+        if (br < bc || (br == bc && ir <= ic)) return U[upper_tile(T_, br, bc) + ir * 64 + ic];
+        if (br == bc) return U[upper_tile(T_, br, br) + ic * 64 + ir];
+        return Ut[upper_tile(T_, bc, br) + ir * 64 + ic];  // (Ut tile) = (U tile)^T
+    }
+}
+
+// MODE (timing-only ablations, tools/k2_modes.py): 1 = loads and keys, no
+// sort; 2 = sort of synthetic keys, no loads
+template <int NT, int KPT, int NT_SUM, bool TR, int MODE = 0>
+__global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
+                                                const double *__restrict__ Ut,
+                                                const double *__restrict__ dg_in, int T_, int n,
+                                                int N, int64_t k, double *__restrict__ scores,
+                                                double *__restrict__ diag) {
+    static_assert(NT_SUM % NT == 0 && NT % 64 == 0, "summation shape");
+    extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // N
+    __shared__ double red[NT_SUM / 64];
+    const int i = blockIdx.x, tid = threadIdx.x;
+    const double di = TR ? dg_in[i] : u_at(U, T_, i, i);
+    if (tid == 0) diag[i] = di;
+    // distances, element e = tid + NT q (consecutive lanes, consecutive
+    // columns: coalesced row reads), through LDS into the blocked layout
+    double *kd = reinterpret_cast<double *>(keys);
+    bool nan = false;
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+        const int e = tid + NT * q;
+        double x = __builtin_inf();  // padding sorts after every real value
+        if (MODE == 2) {
+            x = (double)((e * 2654435761u + i) & 0xFFFFF);
+        } else if (e < n) {
+            const double t = di + (TR ? dg_in[e] : u_at(U, T_, e, e));
+            const double g2 = 2.0 * k2_g<TR>(U, Ut, T_, i, e);
+            x = t - g2;
+            x = x == 0.0 ? 0.0 : x;  // -0 == +0 (v1's dkey)
+            nan |= x != x;
+        }
+        kd[e] = x;
+    }
+    if (MODE == 1) {
+        if (kd[tid] == 1.2345) scores[i] = kd[tid];  // keep the loads
+        return;
+    }
+    __syncthreads();
+    double dv[KPT];
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) dv[q] = kd[tid * KPT + q];
+    double sum;
+    if (!__syncthreads_or(nan)) {  // (the barrier also orders kd[] reads before the sort's writes)
+        k2_sort<double, NT, KPT>(dv, reinterpret_cast<double *>(keys), N, tid);
+        sum = k2_sum<double, NT, NT_SUM>(reinterpret_cast<const double *>(keys), k, tid, red);
+    } else {  // a NaN in the row: v1's order-preserving keys, NaN last
+        uint64_t v[KPT];
+#pragma unroll
+        for (int q = 0; q < KPT; ++q)
+            v[q] = tid * KPT + q < n ? dkey(dv[q]) : ~0ULL;
+        k2_sort<uint64_t, NT, KPT>(v, keys, N, tid);
+        sum = k2_sum<uint64_t, NT, NT_SUM>(keys, k, tid, red);
+    }
+    if (tid == 0) scores[i] = (k > 0) ? sum : 0.0;
+}
+
+// Ut (the off-diagonal upper tiles transposed) and the contiguous diagonal,
+// for K2's coalesced row reads at large n; one 64x64 tile per block through LDS
+__global__ __launch_bounds__(256) void k_transpose(const double *__restrict__ U, int T_,
+                                                   double *__restrict__ Ut,
+                                                   double *__restrict__ dg) {
+    __shared__ double t[64][65];
+    int bi, bj;
+    tri_decode(blockIdx.x, T_, bi, bj);
+    const double *src = U + (int64_t)blockIdx.x * 4096;
+    if (bi == bj) {
+        if (threadIdx.x < 64) dg[bi * 64 + threadIdx.x] = src[threadIdx.x * 65];
+        return;
+    }
+    for (int e = threadIdx.x; e < 4096; e += 256) t[e >> 6][e & 63] = src[e];
+    __syncthreads();
+    double *dst = Ut + (int64_t)blockIdx.x * 4096;
+    for (int e = threadIdx.x; e < 4096; e += 256) dst[e] = t[e & 63][e >> 6];
+}
+
 // ---------------------------------------------------------------------------
 // K3: rank_i = #{j : key_j < key_i} + #{j < i : key_j == key_i}; mask = rank < m
 // ---------------------------------------------------------------------------
@@ -1330,10 +1607,84 @@ static int next_pow2(int v) {
     return p;
 }
 
-hipError_t launch_scores(const double *U, int T, int n, int64_t k, double *scores, double *diag,
-                         hipStream_t st) {
+template <int NT, int KPT, int NT_SUM, bool TR>
+static void launch_scores2(const double *U, const double *Ut, const double *dg, int T, int n, int N,
+                           int64_t k, double *scores, double *diag, hipStream_t st) {
+    static const int mode = [] {
+        const char *e = getenv("BK_K2_MODE");  // timing-only ablations (tools/), never tests
+        return e ? atoi(e) : 0;
+    }();
+    const size_t lds = (size_t)N * sizeof(uint64_t);
+    if (mode == 1)
+        hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 1>), dim3(n), dim3(NT), lds, st, U, Ut,
+                           dg, T, n, N, k, scores, diag);
+    else if (mode == 2)
+        hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 2>), dim3(n), dim3(NT), lds, st, U, Ut,
+                           dg, T, n, N, k, scores, diag);
+    else
+        hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR>), dim3(n), dim3(NT), lds, st, U, Ut, dg,
+                           T, n, N, k, scores, diag);
+}
+
+bool scores_transposed(int n) {
+    static const int tmin = [] {
+        const char *e = getenv("BK_K2_TRANSPOSE_MIN_N");  // probe knob
+        return e ? atoi(e) : 2049;
+    }();
+    return n >= tmin;
+}
+
+hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipStream_t st) {
+    hipLaunchKernelGGL(k_transpose, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, st, U, T, Ut,
+                       dg);
+    return hipGetLastError();
+}
+
+hipError_t launch_scores(const double *U, const double *Ut, const double *dg, int T, int n,
+                         int64_t k, double *scores, double *diag, hipStream_t st) {
     const int np2 = next_pow2(n < 2 ? 2 : n);
     const size_t lds = (size_t)np2 * sizeof(uint64_t);
+    static const bool v1 = [] {
+        const char *e = getenv("BK_SCORES");
+        return e && strcmp(e, "v1") == 0;
+    }();
+    static const int kpt_big = [] {  // probe knob: keys per thread above 2048 keys
+        const char *e = getenv("BK_K2_KPT");
+        return e ? atoi(e) : 16;
+    }();
+    if (!v1) {
+        // v2: 256 threads up to 2048 keys (KPT = N / 256), then KPT = 16 (or
+        // 4); the v1 summation shape (256 / 1024 threads) is emulated
+        const int N = np2 < 256 ? 256 : np2;
+        if (Ut) {
+            switch (N) {
+            case 4096:
+                if (kpt_big == 4)
+                    launch_scores2<1024, 4, 1024, true>(U, Ut, dg, T, n, N, k, scores, diag, st);
+                else
+                    launch_scores2<256, 16, 1024, true>(U, Ut, dg, T, n, N, k, scores, diag, st);
+                break;
+            case 8192: launch_scores2<512, 16, 1024, true>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+            default: launch_scores2<1024, 16, 1024, true>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+            }
+            return hipGetLastError();
+        }
+        switch (N) {
+        case 256: launch_scores2<256, 1, 256, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+        case 512: launch_scores2<256, 2, 256, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+        case 1024: launch_scores2<256, 4, 256, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+        case 2048: launch_scores2<256, 8, 256, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+        case 4096:
+            if (kpt_big == 4)
+                launch_scores2<1024, 4, 1024, false>(U, Ut, dg, T, n, N, k, scores, diag, st);
+            else
+                launch_scores2<256, 16, 1024, false>(U, Ut, dg, T, n, N, k, scores, diag, st);
+            break;
+        case 8192: launch_scores2<512, 16, 1024, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+        default: launch_scores2<1024, 16, 1024, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+        }
+        return hipGetLastError();
+    }
     if (np2 <= 2048) {
         hipLaunchKernelGGL(k_scores<256>, dim3(n), dim3(256), lds, st, U, T, n, np2, k, scores,
                            diag);
@@ -1471,6 +1822,33 @@ hipError_t configure_kernels() {
     e = hipFuncSetAttribute((const void *)k_scores<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             131072);
     if (e != hipSuccess) return e;
+    for (const void *kk : {(const void *)k_scores2<256, 16, 1024, false>,
+                           (const void *)k_scores2<512, 16, 1024, false>,
+                           (const void *)k_scores2<1024, 16, 1024, false>,
+                           (const void *)k_scores2<1024, 4, 1024, false>,
+                           (const void *)k_scores2<256, 16, 1024, true>,
+                           (const void *)k_scores2<512, 16, 1024, true>,
+                           (const void *)k_scores2<1024, 16, 1024, true>,
+                           (const void *)k_scores2<1024, 4, 1024, true>,
+                           (const void *)k_scores2<256, 16, 1024, false, 1>,
+                           (const void *)k_scores2<512, 16, 1024, false, 1>,
+                           (const void *)k_scores2<1024, 16, 1024, false, 1>,
+                           (const void *)k_scores2<1024, 4, 1024, false, 1>,
+                           (const void *)k_scores2<256, 16, 1024, false, 2>,
+                           (const void *)k_scores2<512, 16, 1024, false, 2>,
+                           (const void *)k_scores2<1024, 16, 1024, false, 2>,
+                           (const void *)k_scores2<1024, 4, 1024, false, 2>,
+                           (const void *)k_scores2<256, 16, 1024, true, 1>,
+                           (const void *)k_scores2<512, 16, 1024, true, 1>,
+                           (const void *)k_scores2<1024, 16, 1024, true, 1>,
+                           (const void *)k_scores2<1024, 4, 1024, true, 1>,
+                           (const void *)k_scores2<256, 16, 1024, true, 2>,
+                           (const void *)k_scores2<512, 16, 1024, true, 2>,
+                           (const void *)k_scores2<1024, 16, 1024, true, 2>,
+                           (const void *)k_scores2<1024, 4, 1024, true, 2>}) {
+        e = hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+        if (e != hipSuccess) return e;
+    }
     // the masked column sums keep up to BK_MAX_N row offsets in LDS
     for (const void *k : {(const void *)k_mean<double, true, false>,
                           (const void *)k_mean<double, false, false>,

@@ -300,7 +300,7 @@ int bk_roni(bk_ctx *ctx, const double *ww, const double *deltas, int64_t n, int6
 enum bk_kernel_id {
     BK_K_GRAM = 0,     /* K1  fp64-MFMA split-K upper-triangle Gram partials */
     BK_K_REDUCE = 1,   /* K1b fixed-order split-K reduce -> packed upper     */
-    BK_K_EXPAND = 2,   /* reserved: the n x n expansion is fused into K2     */
+    BK_K_EXPAND = 2,   /* K2t k_transpose: large n, K2's coalesced row copy  */
     BK_K_SCORES = 3,   /* K2  distance row, bitonic sort, sum ranks 1..k    */
     BK_K_RANK = 4,     /* K3  selection rank + mask                          */
     BK_K_COMPACT = 5,  /* K3b mask -> ascending sel_idx                      */

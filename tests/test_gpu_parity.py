@@ -259,7 +259,7 @@ def test_timing_api(engine):
     engine.timing_enable(False)
     for k in ("k_gram", "k_reduce", "k_scores", "k_rank", "k_compact", "k_mean"):
         assert t[k]["count"] == 3 and t[k]["avg_ms"] > 0
-    assert "k_expand" not in t  # fused into k_scores (reads the packed upper tiles)
+    assert "k_transpose" not in t  # small n: k_scores reads the packed upper tiles
 
 
 @pytest.mark.parametrize("deterministic", [False, True])

@@ -47,11 +47,14 @@ for (n, d, f, dt, tdt, seed) in [(512, 131072, 153, _lib.BK_F64, torch.float64, 
                                              ctypes.c_void_p(sel.data_ptr()),
                                              ctypes.c_void_p(sc.data_ptr()), None) == 0
             L.bk_synchronize(c)
-        ms, cnt = ctypes.c_double(), ctypes.c_int64()
-        L.bk_timing_read(c, _lib.K["k_scores"], ctypes.byref(ms), ctypes.byref(cnt))
-        out.append((sel.cpu().numpy(), sc.cpu().numpy(), ms.value / max(cnt.value, 1)))
+        tot = 0.0
+        for kname in ("k_scores", "k_transpose"):  # k_transpose: id 2 (v2, large n)
+            ms, cnt = ctypes.c_double(), ctypes.c_int64()
+            L.bk_timing_read(c, _lib.K[kname], ctypes.byref(ms), ctypes.byref(cnt))
+            tot += ms.value / max(cnt.value, 1) if cnt.value else 0.0
+        out.append((sel.cpu().numpy(), sc.cpu().numpy(), tot))
     same = np.array_equal(out[0][1].view(np.int64), out[1][1].view(np.int64)) and \
         np.array_equal(out[0][0], out[1][0])
-    print("n=%5d d=%6d: k_scores base %.4f ms  new %.4f ms  scores+selection bitwise %s"
+    print("n=%5d d=%6d: k_scores(+k_transpose) base %.4f ms  new %.4f ms  scores+selection bitwise %s"
           % (n, d, out[0][2], out[1][2], same), flush=True)
     assert same
