@@ -19,7 +19,8 @@ BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
 BK_ABI_VERSION = 7
 BK_F32_EXACT, BK_F32_MFMA, BK_F32_CERTIFIED = 0, 1, 2
 KERNELS = ["k_gram", "k_reduce", "k_transpose", "k_scores", "k_rank", "k_compact", "k_mean",
-           "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni"]
+           "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni",
+           "k_small"]
 K = {name: i for i, name in enumerate(KERNELS)}
 
 # every symbol include/bk.h declares: name -> (restype, argtypes)
@@ -78,6 +79,7 @@ SIGNATURES = {
     "bk_certified_reruns": (_i64, [_p]),
     "bk_comm_size": (_i, [_p, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "bk_comm_stats": (_i, [_p, _pi64, _pd]),
+    "bk_set_small_path": (_i, [_p, _i]),
 }
 
 _lib = None

@@ -60,7 +60,7 @@ const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_transpo
                                             "k_rank",    "k_compact", "k_mean",   "allreduce",
                                             "k_synth",   "h2d",       "d2h",
                                             "k_aggregate", "k_qsum",  "k_noise",
-                                            "k_roni"};
+                                            "k_roni", "k_small"};
 
 struct DevBuf {
     void *p = nullptr;
@@ -81,6 +81,10 @@ struct bk_ctx {
     // the selection margin of the last finish (K2 diag, K3 boundary scores, K3b record)
     DevBuf diag, bnd, margin;
     DevBuf Ut;  // K2 at large n: transposed off-diagonal tiles + diagonal (k_transpose)
+    // k_small (n <= 128, one launch): its queue counters (zeroed once; every
+    // launch leaves them zero) and the split-K partials
+    DevBuf small_ctr, small_part;
+    int small_on = 1;
     int margin_valid = 0;
     // BK_F32_CERTIFIED: 1 while the exact re-run of a near-tie call is in progress
     int force_exact = 0;
@@ -173,7 +177,7 @@ void bind_epoch(bk_ctx *c) {
     DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,   &c->scores, &c->mask,   &c->sel,
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                      &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut};
+                      &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -423,8 +427,48 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     return BK_OK;
 }
 
+// k_small (bk_small.hip) takes the whole call for Biscotti's deployed shapes:
+// n <= 128 (one 16x16-block grid per wave set), rows aligned for 16-B (fp64)
+// or 8-B (fp32) loads, and d small enough that one launch beats the chain
+bool small_ok(const bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld) {
+    static const int64_t dmax = [] {
+        const char *e = getenv("BK_SMALL_MAX_D");
+        return e ? atoll(e) : (int64_t)262144;
+    }();
+    if (!c->small_on || n > 128 || d > dmax || (ld & 1)) return false;
+    return ((uintptr_t)dX % (dtype == BK_F64 ? 16 : 8)) == 0;
+}
+
+int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld, int64_t f,
+              int64_t *d_sel, double *d_scores, double *d_mean) {
+    const SmallPlan sp = small_plan((int)n, d, c->num_cu);
+    if (!c->small_ctr.p) {
+        CHK(ensure(c->small_ctr, SMALL_CTR_WORDS * sizeof(unsigned)));
+        HIPCHK(hipMemsetAsync(c->small_ctr.p, 0, SMALL_CTR_WORDS * sizeof(unsigned), c->stream));
+    }
+    CHK(ensure(c->small_part, (size_t)sp.P * sp.nblk * 256 * sizeof(double)));
+    CHK(ensure(c->U, (size_t)bk_upper_elems(n) * sizeof(double)));
+    CHK(ensure(c->diag, (size_t)n * sizeof(double)));
+    CHK(ensure(c->margin, 8 * sizeof(double)));
+    double *sc = d_scores;
+    if (!sc) {
+        CHK(ensure(c->scores, (size_t)n * sizeof(double)));
+        sc = (double *)c->scores.p;
+    }
+    CHK(timed(c, BK_K_SMALL, [&] {
+        return launch_small(dX, dtype, ld, (int)n, d, (int)f, sp, (double *)c->small_part.p,
+                            (double *)c->U.p, sc, (double *)c->diag.p, d_sel, d_mean,
+                            (double *)c->margin.p, (unsigned *)c->small_ctr.p, c->num_cu,
+                            c->stream);
+    }));
+    c->margin_valid = 1;
+    return BK_OK;
+}
+
 int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld, int64_t f,
                int64_t *d_sel, double *d_scores, double *d_mean) {
+    if (small_ok(c, dX, dtype, n, d, ld))
+        return run_small(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
     Plan pl;
     const size_t usz = (size_t)bk_upper_elems(n);
     CHK(ensure(c->U, usz * sizeof(double)));
@@ -586,6 +630,8 @@ int read_margin(bk_ctx *c, double (&mg)[8]) {
     if (!c->margin_valid) return fail(BK_EINVAL, "no Multi-Krum call on this context yet");
     HIPCHK(hipMemcpyAsync(mg, c->margin.p, sizeof mg, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (mg[2] == 2.0)
+        return fail(BK_EHIP, "k_small: a hand-off wait timed out; the last call's outputs are invalid");
     return BK_OK;
 }
 
@@ -663,6 +709,7 @@ int bk_create(bk_ctx **out, int device) {
     if (const char *v = getenv("BK_GRAM"))
         if (strcmp(v, "v1") == 0) c->gram_variant = 1;
     if (const char *v = getenv("BK_GRAM_MODE")) c->gram_mode = atoi(v);
+    if (const char *v = getenv("BK_SMALL")) c->small_on = atoi(v) != 0;
     e = configure_kernels();
     if (e == hipSuccess) e = configure_aggregate_kernels();
     if (e != hipSuccess) {
@@ -683,7 +730,7 @@ void bk_destroy(bk_ctx *c) {
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->scores,
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                          &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut};
+                          &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part};
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
@@ -1109,6 +1156,14 @@ int bk_selection_margin_record(bk_ctx *c, double *record) {
 }
 
 int64_t bk_certified_reruns(bk_ctx *c) { return c ? c->certified_reruns : 0; }
+
+int bk_set_small_path(bk_ctx *c, int on) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->small_on != (on ? 1 : 0)) ++c->ws_epoch;  // captured graphs baked the other path in
+    c->small_on = on ? 1 : 0;
+    return BK_OK;
+}
 
 // ---- one process, G GPUs --------------------------------------------------
 }  // extern "C"

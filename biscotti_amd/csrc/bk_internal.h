@@ -115,6 +115,16 @@ hipError_t configure_aggregate_kernels();
 hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, const double *yv,
                        const double *ww, const double *deltas, int64_t n, int64_t ld,
                        unsigned int *cnt, double *scores, hipStream_t st);
+// bk_small.hip: the whole Multi-Krum of a small batch (n <= 128) in one launch
+struct SmallPlan {
+    int nb16 = 0, nblk = 0, kc = 0, P = 0, Q = 0, nS = 0, C = 0;
+};
+SmallPlan small_plan(int n, int64_t d, int num_cu);
+constexpr int SMALL_CTR_WORDS = 8;
+hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
+                        const SmallPlan &p, double *part, double *U, double *scores, double *diag,
+                        int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
+                        hipStream_t st);
 hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, int64_t c0,
                         const int64_t *perm, const SynthParams &P, hipStream_t st);
 

@@ -288,6 +288,10 @@ class Engine:
         out["k"] = int(out["k"])
         return out
 
+    def set_small_path(self, on=True):
+        """n <= 128: the one-launch k_small path (default) or the general chain."""
+        check(lib().bk_set_small_path(self._ctx, 1 if on else 0))
+
     def certified_reruns(self):
         return int(lib().bk_certified_reruns(self._ctx))
 

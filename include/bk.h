@@ -97,6 +97,13 @@ int bk_multikrum(bk_ctx *ctx, const void *X, int where, int dtype, int64_t n, in
 int bk_multikrum_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
                         int64_t ld, int64_t f, int64_t *d_sel_idx, double *d_scores,
                         double *d_mean);
+/* Small batches (n <= 128, d <= 262144, rows aligned for 16-B fp64 / 8-B fp32
+ * loads: Biscotti's deployed shapes, configs A and B) run as ONE launch,
+ * k_small: split-K Gram, reduce, scores, selection and mean pulled as work
+ * items from a queue in dependency order (no co-residency assumed).  The same
+ * results as the general path: selection, and the mean bitwise; scores within
+ * rounding (another split of the Gram).  on = 0 forces the general path. */
+int bk_set_small_path(bk_ctx *ctx, int on);
 /* Replay bk_multikrum_device as a hipGraph (one captured launch sequence per
  * call signature: pointers, shape, f; up to 4 cached).  The first call of a
  * signature runs eagerly, the second captures, later ones replay; graphs are
@@ -313,7 +320,8 @@ enum bk_kernel_id {
     BK_K_QSUM = 12,      /* K5  quantised int64 sum (bk_quantized_sum_device)  */
     BK_K_NOISE = 13,     /* K6  noise application (bk_noise_apply_device)      */
     BK_K_RONI = 14,      /* K7  RONI counts + scores (bk_roni*)                 */
-    BK_NUM_KERNELS = 15
+    BK_K_SMALL = 15,     /* K1..K4 fused in one launch for n <= 128 (k_small)   */
+    BK_NUM_KERNELS = 16
 };
 int bk_timing_enable(bk_ctx *ctx, int on);   /* all kernels; clears accumulated timings */
 /* Time only the kernels whose bit (1u << kernel_id) is set: every timed kernel

@@ -44,7 +44,7 @@ def test_abi_version_and_names():
     assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 7
     assert L.bk_kernel_name(0) == b"k_gram"
     assert L.bk_kernel_name(99) == b"?"
-    assert len(_lib.KERNELS) == 15
+    assert len(_lib.KERNELS) == 16
     for i, name in enumerate(_lib.KERNELS):
         assert L.bk_kernel_name(i) == name.encode()
 
@@ -124,6 +124,7 @@ def test_null_and_bad_arguments_do_not_crash():
     assert L.bk_certified_reruns(None) == 0
     assert L.bk_comm_size(None, None, None) == _lib.BK_EINVAL
     assert L.bk_comm_stats(None, None, None) == _lib.BK_EINVAL
+    assert L.bk_set_small_path(None, 1) == _lib.BK_EINVAL
     assert L.bk_multikrum_sharded_device(None, None, 0, 10, 0, 0, 2, None, None,
                                          None) == _lib.BK_EINVAL
 

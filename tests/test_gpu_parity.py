@@ -249,7 +249,7 @@ def test_validator_end_to_end(engine, oracle):
 
 
 def test_timing_api(engine):
-    n, d, f = 128, 4096, 30
+    n, d, f = 129, 4096, 30  # n > 128: the general chain (k_small takes n <= 128)
     X = torch.empty((n, d), dtype=torch.float64, device="cuda")
     engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 1, 30)
     engine.timing_enable(True)

@@ -1,0 +1,136 @@
+"""k_small (bk_small.hip): the whole Multi-Krum of an n <= 128 batch in ONE
+launch -- Biscotti's deployed verifier shapes (config A creditcard n <= 10,
+d = 25; config B mnist 100 x 7,850).  Checked on the MI355X:
+
+* every golden with n <= 128 through the device entry: the selection equals
+  the reference's (bit-exact) wherever the margin certifies it, scores within
+  1e-9, mean within the §8(d) bound, and the margin record matches its
+  definition;
+* against the general six-launch chain on the same batch: same selection,
+  the mean BITWISE (same ascending order of adds), scores within rounding;
+* ragged shapes: n = 2..128, d from 1 to non-multiples of 8, fp32 rows;
+* hundreds of back-to-back launches over alternating shapes (the queue
+  counters reset themselves), run-to-run bitwise determinism, and no hand-off
+  wait ever times out (bk_selection_margin would report BK_EHIP).
+"""
+import numpy as np
+import pytest
+
+import golden_util as GU
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from biscotti_amd import _lib  # noqa: E402
+
+
+def _run(e, X, f, scores=True, mean=True):
+    n, d = X.shape
+    dt = _lib.BK_F32 if X.dtype == torch.float32 else _lib.BK_F64
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    sc = torch.empty(n, dtype=torch.float64, device="cuda") if scores else None
+    mn = torch.empty(d, dtype=torch.float64, device="cuda") if mean else None
+    e.multikrum_device_ptr(X.data_ptr(), dt, n, d, X.stride(0), f, sel.data_ptr(),
+                           sc.data_ptr() if sc is not None else None,
+                           mn.data_ptr() if mn is not None else None)
+    e.synchronize()
+    return (sel.cpu().numpy(), sc.cpu().numpy() if sc is not None else None,
+            mn.cpu().numpy() if mn is not None else None)
+
+
+def _timed_kernels(e, X, f):
+    e.timing_enable(True)
+    _run(e, X, f)
+    t = e.timing_read()
+    e.timing_enable(False)
+    return t
+
+
+SMALL = [k for k in GU.small_cases() if GU.C.case_params(k)["n"] <= 128
+         and not GU.C.case_params(k)["error"]]
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_small_goldens_one_launch(name, engine, oracle):
+    Xh, p = GU.build_input(name, oracle)
+    n, d, f = p["n"], p["d"], p["f"]
+    X = torch.from_numpy(np.ascontiguousarray(Xh)).cuda()
+    t = _timed_kernels(engine, X, f)
+    assert "k_small" in t and "k_gram" not in t, t  # the one-launch path ran
+    sel, sc, mean = _run(engine, X, f)
+    g = GU.load(name)
+    mg = engine.selection_margin()
+    GU.check_margin(mg, sc, g["sq"], n, f, d)
+    assert mg["near_tie"] == p["tie"]
+    if not mg["near_tie"]:
+        assert np.array_equal(sel, g["sel"])
+    GU.check_scores(sc, g, rel=1e-9)
+    if not p["tie"]:
+        GU.check_mean(mean, g, GU.manifest()[name])
+
+
+@pytest.mark.parametrize("n,d,f,dtype", [
+    (2, 1, 1, torch.float64), (3, 7, 1, torch.float64), (10, 25, 2, torch.float64),
+    (16, 8, 5, torch.float64), (17, 1001, 5, torch.float64), (64, 4096, 20, torch.float64),
+    (100, 7850, 30, torch.float64), (100, 7850, 50, torch.float64), (127, 333, 40, torch.float64),
+    (128, 65536, 38, torch.float64), (100, 7852, 30, torch.float32), (33, 1003, 10, torch.float32),
+    (128, 262144, 38, torch.float64)])
+def test_small_matches_general_chain(engine, oracle, n, d, f, dtype):
+    from biscotti_amd.krum import Engine
+    gen = Engine(0)
+    gen.set_stream(torch.cuda.current_stream().cuda_stream)
+    gen.set_small_path(False)
+    try:
+        Xh = oracle.synth(n, d, 300 + n + d, max(1, f // 2),
+                          dtype=np.float32 if dtype == torch.float32 else np.float64)
+        X = torch.from_numpy(Xh).cuda()
+        a = _run(engine, X, f)
+        b = _run(gen, X, f)
+        assert "k_small" not in _timed_kernels(gen, X, f)
+        assert np.array_equal(a[0], b[0])
+        assert np.array_equal(a[2].view(np.uint8), b[2].view(np.uint8))  # mean: same order
+        scale = max(1e-300, float(np.max(np.abs(b[1]))))
+        assert float(np.max(np.abs(a[1] - b[1]))) <= 1e-12 * scale
+        osel, osc, omean = oracle.krum(Xh, f)
+        assert np.array_equal(a[0], osel)
+        assert float(np.max(np.abs(a[1] - osc))) <= 1e-9 * max(1e-300, float(np.max(np.abs(osc))))
+    finally:
+        gen.close()
+
+
+def test_small_many_launches_alternating_shapes(engine, oracle):
+    """Back-to-back launches over alternating shapes, without syncs in between
+    (the queue counters reset at the end of every launch, in stream order);
+    every result bitwise equal to a lone call's."""
+    shapes = [(10, 25, 2), (100, 7850, 30), (128, 1000, 60), (37, 513, 11)]
+    data, ref = [], []
+    for i, (n, d, f) in enumerate(shapes):
+        X = torch.from_numpy(oracle.synth(n, d, 70 + i, f)).cuda()
+        data.append(X)
+        ref.append(_run(engine, X, f))
+    outs = []
+    for r in range(60):
+        i = r % len(shapes)
+        n, d, f = shapes[i]
+        X = data[i]
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        sc = torch.empty(n, dtype=torch.float64, device="cuda")
+        mn = torch.empty(d, dtype=torch.float64, device="cuda")
+        engine.multikrum_device_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr(),
+                                    sc.data_ptr(), mn.data_ptr())
+        outs.append((i, sel, sc, mn))
+    engine.synchronize()
+    for i, sel, sc, mn in outs:
+        for u, v in zip((sel.cpu().numpy(), sc.cpu().numpy(), mn.cpu().numpy()), ref[i]):
+            assert np.array_equal(u.view(np.uint8), v.view(np.uint8))
+    engine.selection_margin()  # raises (BK_EHIP) if any hand-off wait had timed out
+
+
+def test_small_optional_outputs(engine, oracle):
+    Xh = oracle.synth(100, 7850, 5, 30)
+    X = torch.from_numpy(Xh).cuda()
+    full = _run(engine, X, 30)
+    s1, _, _ = _run(engine, X, 30, scores=False, mean=False)
+    assert np.array_equal(s1, full[0])
+    s2, _, m2 = _run(engine, X, 30, scores=False)
+    assert np.array_equal(m2.view(np.uint8), full[2].view(np.uint8))
