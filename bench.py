@@ -72,7 +72,7 @@ def single_call(step, eng, barrier, world, dev, calls=7, idle_s=0.2):
     whole step (max over ranks) and of K1 (HIP events on libbk's stream)."""
     import torch
     import torch.distributed as tdist
-    eng.timing_select(["k_gram"])
+    eng.timing_select(["k_gram", "k_small"])
     steps_ms, k1_ms = [], []
     prev = 0.0
     for _ in range(calls):
@@ -88,7 +88,8 @@ def single_call(step, eng, barrier, world, dev, calls=7, idle_s=0.2):
             tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
             t = float(tt.item())
         steps_ms.append(t)
-        tot = eng.timing_read().get("k_gram", {"total_ms": prev})["total_ms"]
+        tr = eng.timing_read()
+        tot = tr.get("k_gram", tr.get("k_small", {"total_ms": prev}))["total_ms"]
         k1_ms.append(tot - prev)
         prev = tot
     eng.timing_select([])
@@ -261,6 +262,53 @@ def graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt):
     return res
 
 
+def small_variant(eng, dev, steps=500, warmup=50):
+    """Config B (mnist softmax: 100 x 7,850 fp64, f = 30), the
+    shape Biscotti's verifiers actually run, device-resident: the one-launch
+    k_small path (bk_set_small_path, default for n <= 128) against the general
+    six-launch chain on the same batch; parity against the B golden."""
+    import torch
+    from biscotti_amd import _lib
+    w = WORKLOADS["B_mnist"]
+    n, d, f = w["n"], w["d"], w["f"]
+    m = n - f
+    X = torch.empty((n, d), dtype=torch.float64, device=dev)
+    eng.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, w["seed"], w["nbyz"],
+                       flags=w.get("flags", 0))
+    sel = torch.empty(m, dtype=torch.int64, device=dev)
+    sc = torch.empty(n, dtype=torch.float64, device=dev)
+    mean = torch.empty(d, dtype=torch.float64, device=dev)
+
+    def step():
+        eng.multikrum_device_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr(),
+                                 sc.data_ptr(), mean.data_ptr())
+
+    flops = n * (n + 1) * d
+    bytes_alg = (n + m) * d * 8 + 8 * d
+    t_floor = max(flops / (PEAK_TFLOPS["f64"] * 1e12), bytes_alg / (PEAK_HBM_GBS * 1e9)) * 1e3
+    res = {"n": n, "d": d, "f": f, "steps": steps}
+    for label, on in (("one_launch", True), ("general_chain", False)):
+        eng.set_small_path(on)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        res[label] = {"ms_per_step": round(ms, 5), "GB_per_s": round(n * d * 8 / (ms * 1e-3) / 1e9, 2),
+                      "step_roofline": {"t_floor_ms": round(t_floor, 5),
+                                        "bound": "hbm" if bytes_alg / PEAK_HBM_GBS > flops / PEAK_TFLOPS["f64"] / 1e3 else "mfma",
+                                        "frac": round(t_floor / ms, 4)},
+                      "parity": golden_check("B_mnist", sel.cpu().numpy(), mean.cpu().numpy(), 0, d)}
+    eng.set_small_path(True)
+    res["ms_per_step"] = res["one_launch"]["ms_per_step"]
+    res["value"] = res["one_launch"]["GB_per_s"]
+    del X
+    return res
+
+
 def golden_check(name, sel_host, mean_local, c0, dl):
     path = os.path.join(REPO, "tests", "golden", name + ".npz")
     if not os.path.exists(path):
@@ -268,6 +316,12 @@ def golden_check(name, sel_host, mean_local, c0, dl):
     g = np.load(path, allow_pickle=False)
     ok = bool(np.array_equal(np.sort(sel_host), g["sel"]))
     res = {"selected_set": "match" if ok else "MISMATCH"}
+    if "mean" in g.files and mean_local is not None and c0 == 0 and dl == len(g["mean"]):
+        man = json.load(open(os.path.join(REPO, "tests", "golden", "cases.json")))
+        scale = man[name]["mean_scale"]
+        err = float(np.max(np.abs(mean_local - g["mean"])))
+        res["mean_max_err_rel"] = err / scale
+        res["mean"] = "match" if err <= 1e-9 * scale else "MISMATCH"
     if "mean_cols" in g.files and mean_local is not None:
         cols = g["mean_cols"]
         msk = (cols >= c0) & (cols < c0 + dl)
@@ -408,9 +462,10 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    # the roofline kernel (K1) is timed live with HIP events on libbk's stream;
-    # the other kernels are not, so the timed region carries no extra events
-    eng.timing_select(["k_gram"])
+    # the roofline kernel (K1; k_small, the one-launch path, for n <= 128) is
+    # timed live with HIP events on libbk's stream; the other kernels are not,
+    # so the timed region carries no extra events
+    eng.timing_select(["k_gram", "k_small"])
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
@@ -515,7 +570,8 @@ def main():
 
     # roofline of the dominant kernel (K1, fp64 MFMA): algorithmic flops per
     # launch = n(n+1) * d_local (symmetric Gram incl. diagonal)
-    g = kt.get("k_gram", {"avg_ms": float("nan")})
+    k1name = "k_gram" if "k_gram" in kt else "k_small"
+    g = kt.get(k1name, {"avg_ms": float("nan")})
     flops = n * (n + 1) * dl
     achieved = flops / (g["avg_ms"] * 1e-3) / 1e12
     peak = PEAK_TFLOPS["f64"]  # fp32 inputs are widened onto the fp64 MFMA path
@@ -536,7 +592,7 @@ def main():
             traffic = None
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": "k_gram", "kernel_avg_ms": round(g["avg_ms"], 4),
+            "kernel": k1name, "kernel_avg_ms": round(g["avg_ms"], 4),
             "flops_per_launch": flops}
 
     # the whole step against its floor: t_floor = max(flops_alg / fp64
@@ -590,7 +646,7 @@ def main():
                 "krum.go:100-166): the clock ramp a verifier sees",
         "ms": round(sc_step, 4), "GB_per_s": round(sc_gbs, 3),
         "k_gram_ms": round(sc_k1, 4),
-        "k_gram_frac": round(flops / (sc_k1 * 1e-3) / 1e12 / peak, 4),
+        "k_gram_frac": round(flops / (sc_k1 * 1e-3) / 1e12 / peak, 4) if sc_k1 > 0 else None,
         "step_roofline_frac": round(max(t_mfma, t_hbm) / sc_step, 4),
         "calls_ms": [round(x, 4) for x in sc_all]}
 
@@ -616,6 +672,9 @@ def main():
 
     if rank == 0 and world == 1 and not emu and not a.no_next_rows and w["dtype"] == "f64":
         out["next_rows"] = next_rows(eng, X, n, d, sel, m)
+
+    if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD:
+        out.setdefault("variants", {})["B_mnist"] = small_variant(eng, dev)
 
     if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD and not a.no_graph_probe:
         out["hip_graph"] = graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt)

@@ -428,15 +428,17 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
 }
 
 // k_small (bk_small.hip) takes the whole call for Biscotti's deployed shapes:
-// n <= 128 (one 16x16-block grid per wave set), rows aligned for 16-B (fp64)
-// or 8-B (fp32) loads, and d small enough that one launch beats the chain
+// n <= 128 (one 16x16-block grid per wave set) and d small enough that one
+// launch beats the chain
 bool small_ok(const bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld) {
     static const int64_t dmax = [] {
         const char *e = getenv("BK_SMALL_MAX_D");
-        return e ? atoll(e) : (int64_t)262144;
+        return e ? atoll(e) : (int64_t)32768;  // P = d / 64 partials: <= 4 load rounds in R
     }();
-    if (!c->small_on || n > 128 || d > dmax || (ld & 1)) return false;
-    return ((uintptr_t)dX % (dtype == BK_F64 ? 16 : 8)) == 0;
+    (void)dX;
+    (void)dtype;
+    (void)ld;  // unaligned rows take k_small's scalar-load variant
+    return c->small_on && n <= 128 && d <= dmax;
 }
 
 int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld, int64_t f,
@@ -455,13 +457,36 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
         CHK(ensure(c->scores, (size_t)n * sizeof(double)));
         sc = (double *)c->scores.p;
     }
+    long long *trace = nullptr;
+    const int items = sp.P + sp.Q + sp.nS + (d_mean ? sp.C : 0);
+    const char *tfile = getenv("BK_SMALL_TRACE");  // debug: per-item timeline
+    if (tfile) {
+        CHK(ensure(c->trace, (size_t)items * 6 * sizeof(long long)));
+        HIPCHK(hipMemsetAsync(c->trace.p, 0, (size_t)items * 6 * sizeof(long long), c->stream));
+        trace = (long long *)c->trace.p;
+    }
     CHK(timed(c, BK_K_SMALL, [&] {
         return launch_small(dX, dtype, ld, (int)n, d, (int)f, sp, (double *)c->small_part.p,
                             (double *)c->U.p, sc, (double *)c->diag.p, d_sel, d_mean,
                             (double *)c->margin.p, (unsigned *)c->small_ctr.p, c->num_cu,
-                            c->stream);
+                            c->stream, trace);
     }));
     c->margin_valid = 1;
+    if (tfile) {
+        std::vector<long long> h((size_t)items * 6 + 5);
+        h[0] = items;
+        h[1] = sp.P;
+        h[2] = sp.Q;
+        h[3] = sp.nS;
+        h[4] = d_mean ? sp.C : 0;
+        HIPCHK(hipMemcpyAsync(h.data() + 5, trace, (size_t)items * 6 * sizeof(long long),
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (FILE *fp = fopen(tfile, "ab")) {
+            fwrite(h.data(), sizeof(long long), h.size(), fp);
+            fclose(fp);
+        }
+    }
     return BK_OK;
 }
 

@@ -120,11 +120,11 @@ struct SmallPlan {
     int nb16 = 0, nblk = 0, kc = 0, P = 0, Q = 0, nS = 0, C = 0;
 };
 SmallPlan small_plan(int n, int64_t d, int num_cu);
-constexpr int SMALL_CTR_WORDS = 8;
+constexpr int SMALL_CTR_WORDS = 30 * 32;  // 30 queue lines of 128 B (bk_small.hip)
 hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
-                        hipStream_t st);
+                        hipStream_t st, long long *trace = nullptr);
 hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, int64_t c0,
                         const int64_t *perm, const SynthParams &P, hipStream_t st);
 

@@ -11,17 +11,21 @@
 //   G items  (P of them)  split-K Gram partial of d/P columns: every upper
 //                          16x16 block of the (n <= 128) Gram, fp64 MFMA
 //   R items  (4 per block) fixed-order sum of the P partials -> packed upper U
-//   S items  (4 rows each) one wave per row: distances, register bitonic sort
-//                          (k2_*), sum of ranks 1..k in K2's exact shape; the
-//                          last S item to finish (arrival counter) ranks the
-//                          scores, compacts the selection, writes the margin
+//   S items  (one per row) distances, sort by counting, sum of ranks 1..k in
+//                          K2's exact shape; the last S item to finish (its
+//                          arrival add returns n - 1) ranks the scores,
+//                          compacts the selection, writes the margin
 //   M items  (256 columns) mean of the selected rows, ascending (K4's order)
 //
-// An item only waits (a relaxed poll, then an agent-scope acquire) for items
-// dequeued BEFORE it, and a dequeued item's workgroup is running, so the queue
-// always drains: no co-residency is assumed (MI355X_MICROARCH.md, "Workgroup
-// dispatch").  Producers publish with every wave's vmcnt(0), a barrier, an
-// agent release fence and a relaxed atomic add (the guide's "Valid forms").
+// An item only waits (a relaxed sc1 poll of a counter) for items dequeued
+// BEFORE it, and a dequeued item's workgroup is running, so the queue always
+// drains: no co-residency is assumed (MI355X_MICROARCH.md, "Workgroup
+// dispatch").  Hand-offs are the guide's write-through form ("Valid forms",
+// table row 1): EVERY store of handed-off bytes is an sc1 store (agent-scope
+// relaxed atomic store), every storing wave drains vmcnt(0), a workgroup
+// barrier, then one lane's agent-scope atomic add; EVERY load of them is an
+// sc1 load.  No release / acquire fences: a buffer_wbl2 writes back the XCD's
+// dirty L2 (~6.5 us with fresh data), which cost the first version 85 us.
 // The last workgroup to exit resets the counters for the next launch.  A wait
 // gives up after ~1 s and raises an error word instead of hanging the GPU.
 // Results are deterministic: every sum has a fixed order.
@@ -34,7 +38,17 @@
 
 namespace bk {
 
-enum { C_HEAD = 0, C_G = 1, C_R = 2, C_S = 3, C_SEL = 4, C_EXIT = 5, C_ERR = 6 };
+// queue words, each on a 128-B line of its own: the item head, the arrival
+// counters of the G, R and S phases, the exit count, the error word; then the
+// "phase done" flags F_G, F_R, F_SEL, each replicated once per XCD (a waiting
+// workgroup polls its own XCD's copy: 1/8 of the pollers on any line)
+enum { C_HEAD = 0, C_G = 1, C_R = 2, C_S = 3, C_EXIT = 4, C_ERR = 5, F_G = 6, F_R = 14, F_SEL = 22,
+       C_LINES = 30 };
+#ifndef BK_SMALL_KC
+#define BK_SMALL_KC 64
+#endif
+constexpr int SMALL_KC = BK_SMALL_KC;  // columns per G item (groups of 8)
+constexpr int SMALL_GR = SMALL_KC / 2;  // 16-B granules per staged row
 
 struct SmallArgs {
     const void *X;
@@ -43,40 +57,106 @@ struct SmallArgs {
     double *part, *U, *scores, *diag, *mean, *margin;
     int64_t *sel;
     unsigned *ctr;
+    long long *trace;  // debug (BK_SMALL_TRACE): per item {start, waited, end, hw id,
+                       // shader clock at start, at end}
 };
 
 __device__ __forceinline__ unsigned ctr_load(const unsigned *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// wait until *p >= target (lane 0 polls), then acquire for the whole workgroup
-__device__ __forceinline__ void wg_wait(unsigned *p, unsigned target, unsigned *err) {
+// the handed-off bytes: sc1 (write-through) stores and sc1 loads
+template <typename V>
+__device__ __forceinline__ void st1(V *p, V v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename V>
+__device__ __forceinline__ V ld1(const V *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// G_ij from the packed upper tiles (u_at) with sc1 loads
+__device__ __forceinline__ double u_at1(const double *U, int T, int r, int c) {
+    const int br = r >> 6, bc = c >> 6, ir = r & 63, ic = c & 63;
+    if (br < bc || (br == bc && ir <= ic)) return ld1(U + upper_tile(T, br, bc) + ir * 64 + ic);
+    return ld1(U + upper_tile(T, bc, br) + ic * 64 + ir);
+}
+
+__device__ __forceinline__ unsigned *cline(unsigned *ctr, int line) { return ctr + 32 * line; }
+
+__device__ __forceinline__ int xcc_id() {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return (int)(x & 7);
+}
+
+// wait for a phase's flag (lane 0 polls this XCD's copy), then the workgroup
+// goes on: its loads of the handed-off bytes are sc1 loads, after this barrier
+__device__ __forceinline__ void wg_wait_flag(unsigned *ctr, int flag) {
     if (threadIdx.x == 0) {
+        const unsigned *p = cline(ctr, flag + xcc_id());
         uint64_t spins = 0;
-        while (ctr_load(p) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1ull << 23)) {  // ~1 s: never hang the GPU on a broken hand-off
-                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (ctr_load(p) == 0u) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1ull << 24)) {  // ~1 s: never hang the GPU on a broken hand-off
+                __hip_atomic_fetch_or(cline(ctr, C_ERR), 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 }
 
-// publish this workgroup's stores, then count; returns the counter's old value
-__device__ __forceinline__ unsigned wg_signal(unsigned *p, unsigned *s_old) {
+// every wave drains its sc1 stores, then one lane counts the arrival; the
+// workgroup whose add returns last - 1 sees every other producer's bytes
+// (the guide's row 1: the last adder, told by the value its add returned)
+__device__ __forceinline__ bool wg_arrive(unsigned *ctr, int counter, unsigned last,
+                                          unsigned *s_old) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        *s_old = __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)
+        *s_old = __hip_atomic_fetch_add(cline(ctr, counter), 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return *s_old == last - 1;
+}
+
+// the last arriver raises a phase flag on every XCD's copy (one wave
+// instruction, 8 lanes, sc1 stores), after its own stores have drained
+__device__ __forceinline__ void wg_raise(unsigned *ctr, int flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 8) st1(cline(ctr, flag + (int)threadIdx.x), 1u);
+}
+
+// F_SEL carries the selection itself: rows 63w .. 63w+62 in bits 0..62 of
+// u64 word w (w < 3) of every XCD's flag line, bit 63 set in each word; a
+// word is one 8-B sc1 store (single-copy atomic), and a reader that sees bit
+// 63 in all three has the whole mask -- no separate round trip for sel
+__device__ __forceinline__ void sel_raise(unsigned *ctr, const uint64_t (&w)[3]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 24) {
+        uint64_t *line = reinterpret_cast<uint64_t *>(cline(ctr, F_SEL + (int)threadIdx.x / 3));
+        st1(line + threadIdx.x % 3, (uint64_t)(w[threadIdx.x % 3] | (1ull << 63)));
+    }
+}
+__device__ __forceinline__ void sel_wait(unsigned *ctr, uint64_t *mask_lds) {
+    if (threadIdx.x < 3) {
+        const uint64_t *line = reinterpret_cast<const uint64_t *>(cline(ctr, F_SEL + xcc_id()));
+        uint64_t v;
+        uint64_t spins = 0;
+        while (!((v = ld1(line + threadIdx.x)) >> 63)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1ull << 24)) {
+                __hip_atomic_fetch_or(cline(ctr, C_ERR), 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        mask_lds[threadIdx.x] = v & ~(1ull << 63);
     }
     __syncthreads();
-    return *s_old;
 }
 
 // upper 16x16 block b (row-major over bi <= bj) of an NB x NB block grid
@@ -99,22 +179,31 @@ __host__ __device__ constexpr int blk_bj(int b, int NB) {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// the 2 MFMAs of this wave's J-th block per 8-column group; block positions are
-// compile-time, so the fragment array stays in registers
-template <int NB, int W, int J, int NJ>
-__device__ __forceinline__ void small_mma(d4 *acc, const d2v (&fr)[NB]) {
+// sub-step S (0: columns 2g, 1: 2g+1) of this wave's blocks J.. per 8-column
+// group; block positions are compile-time, so the fragments stay in registers
+template <int NB, int W, int S, int J, int NJ>
+__device__ __forceinline__ void small_mma_s(d4 *acc, const d2v (&fr)[NB]) {
     if constexpr (J < NJ) {
         constexpr int b = W + 4 * J;
         constexpr int bi = blk_bi(b, NB), bj = blk_bj(b, NB);
-        acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[bi].x, fr[bj].x, acc[J], 0, 0, 0);
-        acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[bi].y, fr[bj].y, acc[J], 0, 0, 0);
-        small_mma<NB, W, J + 1, NJ>(acc, fr);
+        acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[bi][S], fr[bj][S], acc[J], 0, 0, 0);
+        small_mma_s<NB, W, S, J + 1, NJ>(acc, fr);
     }
 }
+// both sub-steps, blocks interleaved: consecutive MFMAs never share an accumulator
+template <int NB, int W, int J, int NJ>
+__device__ __forceinline__ void small_mma(d4 *acc, const d2v (&fr)[NB]) {
+    small_mma_s<NB, W, 0, J, NJ>(acc, fr);
+    small_mma_s<NB, W, 1, J, NJ>(acc, fr);
+}
 
-template <typename T>
-__device__ __forceinline__ d2v sm_ld2(const T *p) {  // 2 consecutive elements as fp64
-    if constexpr (sizeof(T) == 8) {
+// 2 consecutive elements as fp64; VEC: one 16-B (fp64) / 8-B (fp32) load,
+// else two scalar loads (rows not aligned for it: odd ld, e.g. config A's d = 25)
+template <typename T, bool VEC>
+__device__ __forceinline__ d2v sm_ld2(const T *p) {
+    if constexpr (!VEC) {
+        return d2v{(double)p[0], (double)p[1]};
+    } else if constexpr (sizeof(T) == 8) {
         return *reinterpret_cast<const d2v *>(p);
     } else {
         typedef float f2 __attribute__((ext_vector_type(2)));
@@ -127,61 +216,105 @@ __device__ __forceinline__ d2v sm_ld2(const T *p) {  // 2 consecutive elements a
 // columns [c0, c1).  Lane (rr, g) holds columns 2g, 2g+1 of each 8-column group
 // (the same k permutation for A and B, so the product is exactly X X^T); the
 // output element (row g + 4r, col rr) of a 16x16 block sits in register r.
-template <typename T, int NB, int W>
-__device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int s, int lane) {
+// G item s: the item's rows x 64 columns are staged in LDS once (every load
+// in flight, coalesced 512-B rows; a per-wave re-load of every row-block took
+// 11 us per item), granules XOR-swizzled by (row & 31) so the fragment reads
+// (16 rows x 16 B per lane group) hit distinct banks
+__device__ __forceinline__ int sg_off(int row, int gran) {
+    return row * (SMALL_GR * 16) + ((gran ^ (row & (SMALL_GR - 1))) << 4);
+}
+
+template <typename T, bool VEC, int NB>
+struct SmallStage {
+    static constexpr int ROWS = 16 * NB;
+    static constexpr int PER = (ROWS * SMALL_GR + 255) / 256;  // 16-B granules per thread
+    d2v v[PER];
+    // every load of the item in flight at once (coalesced rows)
+    __device__ __forceinline__ void load(const SmallArgs &a, int s) {
+        const T *X = (const T *)a.X;
+        const int64_t c0 = (int64_t)s * SMALL_KC;
+        const int len = (int)(c0 + SMALL_KC < a.d ? SMALL_KC : a.d - c0);
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int gidx = threadIdx.x + 256 * q;
+            const int row = gidx / SMALL_GR, gr = gidx % SMALL_GR, col = 2 * gr;
+            d2v x = {0.0, 0.0};
+            if (row < ROWS) {
+                const T *p = X + (int64_t)min(row, a.n - 1) * a.ld + c0 + col;
+                if (VEC && col + 1 < len) {
+                    x = sm_ld2<T, true>(p);
+                } else {
+                    x.x = col < len ? (double)p[0] : 0.0;
+                    x.y = col + 1 < len ? (double)p[1] : 0.0;
+                }
+            }
+            v[q] = x;
+        }
+    }
+    // granules [g0, g1) of every row into LDS
+    __device__ __forceinline__ void store(char *tile, int g0, int g1) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int gidx = threadIdx.x + 256 * q;
+            const int row = gidx / SMALL_GR, gr = gidx % SMALL_GR;
+            if (row < ROWS && gr >= g0 && gr < g1) *reinterpret_cast<d2v *>(tile + sg_off(row, gr)) = v[q];
+        }
+    }
+};
+
+// the MFMAs of 8-column groups [t0, t1) of the staged tile
+template <int NB, int W, int NJ>
+__device__ __forceinline__ void small_gram_groups(d4 *acc, const char *tile, int lane, int t0,
+                                                  int t1) {
+    const int rr = lane & 15, g = lane >> 4;
+    if constexpr (NJ > 0) {
+#pragma unroll
+        for (int t = 0; t < SMALL_KC / 8; ++t) {
+            if (t < t0 || t >= t1) continue;
+            d2v fr[NB];
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb)
+                fr[rb] = *reinterpret_cast<const d2v *>(tile + sg_off(16 * rb + rr, 4 * t + g));
+            small_mma<NB, W, 0, NJ>(acc, fr);
+        }
+    }
+}
+
+// G item s: stage the item's columns, the MFMAs, the partials written sc1
+// (staging half the columns and computing it while the other half landed was
+// 1.3 us slower per item: one more barrier, and the item is latency-bound)
+template <typename T, bool VEC, int NB, int W>
+__device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int s, int lane, char *tile,
+                                                SmallStage<T, VEC, NB> &st) {
     constexpr int NBLK = NB * (NB + 1) / 2;
     constexpr int NJ = (NBLK - W + 3) / 4;  // this wave's blocks
-    const T *X = (const T *)a.X;
+    constexpr int NG = SMALL_KC / 8, H = NG / 2;
     const int rr = lane & 15, g = lane >> 4;
-    const int64_t c0 = (int64_t)s * a.kc, c1 = c0 + a.kc < a.d ? c0 + a.kc : a.d;
-    const T *rows[NB];
-#pragma unroll
-    for (int rb = 0; rb < NB; ++rb) {
-        const int r = min(16 * rb + rr, a.n - 1);  // rows past n: duplicates, never read back
-        rows[rb] = X + (int64_t)r * a.ld + c0 + 2 * g;
-    }
     d4 acc[NJ > 0 ? NJ : 1];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
-    const int64_t len = c1 - c0, nfull = len >> 3;
-    d2v fr[NB], nx[NB];
-    if (nfull > 0) {
-#pragma unroll
-        for (int rb = 0; rb < NB; ++rb) fr[rb] = sm_ld2<T>(rows[rb]);
-    }
-    for (int64_t t = 0; t < nfull; ++t) {
-        const int64_t tn = t + 1 < nfull ? t + 1 : t;  // clamped prefetch keeps the loop simple
-#pragma unroll
-        for (int rb = 0; rb < NB; ++rb) nx[rb] = sm_ld2<T>(rows[rb] + tn * 8);
-        small_mma<NB, W, 0, NJ>(acc, fr);
-#pragma unroll
-        for (int rb = 0; rb < NB; ++rb) fr[rb] = nx[rb];
-    }
-    if (len & 7) {  // ragged tail: guarded scalar loads
-        const int64_t k0 = nfull * 8 + 2 * g;
-        const bool v0 = k0 < len, v1 = k0 + 1 < len;
-#pragma unroll
-        for (int rb = 0; rb < NB; ++rb) {
-            fr[rb].x = v0 ? (double)rows[rb][nfull * 8] : 0.0;
-            fr[rb].y = v1 ? (double)rows[rb][nfull * 8 + 1] : 0.0;
-        }
-        small_mma<NB, W, 0, NJ>(acc, fr);
-    }
+    (void)H;
+    st.store(tile, 0, SMALL_GR);
+    __syncthreads();
+    small_gram_groups<NB, W, NJ>(acc, tile, lane, 0, NG);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         double *out = a.part + ((int64_t)s * NBLK + W + 4 * j) * 256;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[(g + 4 * r) * 16 + rr] = acc[j][r];
+        for (int r = 0; r < 4; ++r) st1(out + (g + 4 * r) * 16 + rr, (double)acc[j][r]);
     }
 }
 
-template <typename T, int NB>
-__device__ __forceinline__ void small_gram(const SmallArgs &a, int s, int wave, int lane) {
+template <typename T, bool VEC, int NB>
+__device__ __forceinline__ void small_gram(const SmallArgs &a, int s, int wave, int lane,
+                                           char *tile) {
+    SmallStage<T, VEC, NB> st;
+    st.load(a, s);
     switch (wave) {
-    case 0: small_gram_wave<T, NB, 0>(a, s, lane); break;
-    case 1: small_gram_wave<T, NB, 1>(a, s, lane); break;
-    case 2: small_gram_wave<T, NB, 2>(a, s, lane); break;
-    default: small_gram_wave<T, NB, 3>(a, s, lane); break;
+    case 0: small_gram_wave<T, VEC, NB, 0>(a, s, lane, tile, st); break;
+    case 1: small_gram_wave<T, VEC, NB, 1>(a, s, lane, tile, st); break;
+    case 2: small_gram_wave<T, VEC, NB, 2>(a, s, lane, tile, st); break;
+    default: small_gram_wave<T, VEC, NB, 3>(a, s, lane, tile, st); break;
     }
 }
 
@@ -195,140 +328,132 @@ __device__ __forceinline__ void small_reduce(const SmallArgs &a, int q, int tid,
     const int64_t stride = (int64_t)a.nblk * 256;
     double acc = 0.0;
     int s = ch;
-    for (; s + 28 < a.P; s += 32) {
-        double v[8];
+    for (; s < a.P; s += 4 * 32) {  // 32 loads in flight per thread (P <= 512: 4 rounds at most)
+        double v[32];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(s + 4 * u) * stride];
+        for (int u = 0; u < 32; ++u) v[u] = s + 4 * u < a.P ? ld1(p + (int64_t)(s + 4 * u) * stride) : 0.0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc += v[u];
+        for (int u = 0; u < 32; ++u)
+            if (s + 4 * u < a.P) acc += v[u];
     }
-    for (; s < a.P; s += 4) acc += p[(int64_t)s * stride];
     red[ch][el] = acc;
     __syncthreads();
     if (ch == 0) {
         const double t = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
         const int bi = blk_bi(b, NB), bj = blk_bj(b, NB);
         const int r = 16 * bi + (e >> 4), c = 16 * bj + (e & 15);
-        a.U[upper_tile(a.T, r >> 6, c >> 6) + (r & 63) * 64 + (c & 63)] = t;
-        if (q == 0 && el == 0) a.U[(int64_t)a.T * (a.T + 1) / 2 * 4096] = (double)a.d;
+        st1(a.U + upper_tile(a.T, r >> 6, c >> 6) + (r & 63) * 64 + (c & 63), t);
+        if (q == 0 && el == 0) st1(a.U + (int64_t)a.T * (a.T + 1) / 2 * 4096, (double)a.d);
     }
 }
 
-// S item j: rows 4j + wave, one wave each: K2's distances, sort and sum shape
-// (v1's 256-thread summation emulated: ranks 1 + t', t' = lane + 64 h)
-__device__ __forceinline__ void small_scores(const SmallArgs &a, int j, int wave, int lane,
-                                             double *kbuf) {
-    const int i = 4 * j + wave;
-    if (i >= a.n) return;  // wave-uniform; no barrier below
-    const int n = a.n;
+// S item i: row i with the whole workgroup.  Distances, then a sort by
+// counting (thread t ranks key t & 127 against half of the row, t >> 7; key e
+// goes to position #{keys before it in the (value, index) total order}), then
+// K2's summation with its own 256 threads: thread t sums rank 1 + t, the wave
+// butterfly, the 4 waves in order -- the same sorted array and the same shape,
+// so the score is K2's bitwise (for the same U).
+__device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid, uint64_t *kbuf,
+                                             double *sbuf, int *rk, double *red) {
+    const int n = a.n, lane = tid & 63, wave = tid >> 6;
     const int64_t k = n - a.f - 2 > 0 ? n - a.f - 2 : 0;
-    const double di = u_at(a.U, a.T, i, i);
-    bool nan = false;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int e = lane + 64 * q;
-        double x = __builtin_inf();
-        if (e < n) {
-            x = (di + u_at(a.U, a.T, e, e)) - 2.0 * u_at(a.U, a.T, i, e);
-            x = x == 0.0 ? 0.0 : x;
-            nan |= x != x;
-        }
-        kbuf[e] = x;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    double v[2] = {kbuf[2 * lane], kbuf[2 * lane + 1]};
-    const bool any_nan = __ballot(nan) != 0;
-    double sorted0, sorted1;  // this lane's two sorted keys, as values
-    if (!any_nan) {
-        for (int size = 2; size <= 128; size <<= 1) {  // the all-ascending bitonic of k2_sort
-            if (size == 2) {
-                k2_cas(v[0], v[1]);
-            } else {
-                k2_lane_dispatch<double, 2, 1>(v, (size - 1) >> 1, (lane & ((size >> 1) >> 1)) == 0);
-                for (int st = size >> 2; st >= 2; st >>= 1)
-                    k2_lane_dispatch<double, 2, 0>(v, st >> 1, (lane & (st >> 1)) == 0);
-                k2_cas(v[0], v[1]);
-            }
-        }
-        sorted0 = v[0];
-        sorted1 = v[1];
-    } else {  // a NaN in the row: order-preserving u64 keys, NaN last
-        uint64_t u[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) u[q] = 2 * lane + q < n ? dkey(v[q]) : ~0ULL;
-        for (int size = 2; size <= 128; size <<= 1) {
-            if (size == 2) {
-                k2_cas(u[0], u[1]);
-            } else {
-                k2_lane_dispatch<uint64_t, 2, 1>(u, (size - 1) >> 1, (lane & ((size >> 1) >> 1)) == 0);
-                for (int st = size >> 2; st >= 2; st >>= 1)
-                    k2_lane_dispatch<uint64_t, 2, 0>(u, st >> 1, (lane & (st >> 1)) == 0);
-                k2_cas(u[0], u[1]);
-            }
-        }
-        sorted0 = dkey_inv(u[0]);
-        sorted1 = dkey_inv(u[1]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    kbuf[2 * lane] = sorted0;
-    kbuf[2 * lane + 1] = sorted1;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    double sum = 0.0;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const int r = 1 + lane + 64 * h;
-        double acc = 0.0;
-        if (r <= k) acc += kbuf[r];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-        sum += acc;  // (0 + red_0) + red_1 + ... : K2's order over the 4 virtual waves
-    }
-    if (lane == 0) {
-        a.scores[i] = k > 0 ? sum : 0.0;
-        a.diag[i] = di;
-    }
-}
-
-// the last S item: rank, compact, margin (n <= 128, one workgroup)
-__device__ __forceinline__ void small_select(const SmallArgs &a, int wave, int lane, int *msk,
-                                             double *bnd) {
-    const int n = a.n, m = n - a.f;
-    for (int i = wave; i < n; i += 4) {
-        const double si = a.scores[i];
-        const uint64_t ki = dkey(si);
-        int cnt = 0;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int j = lane + 64 * q;
-            bool before = false;
-            if (j < n) {
-                const uint64_t kj = dkey(a.scores[j]);
-                before = (kj < ki) || (kj == ki && j < i);
-            }
-            cnt += __popcll(__ballot(before));
-        }
-        if (lane == 0) {
-            msk[i] = cnt < m ? 1 : 0;
-            if (cnt == m - 1) bnd[0] = si;
-            if (cnt == m) bnd[1] = si;
-        }
+    const int e = tid & 127, h = tid >> 7;
+    const double di = u_at1(a.U, a.T, i, i);
+    if (h == 0) {
+        uint64_t key = ~0ULL;  // padding sorts last
+        if (e < n) key = dkey((di + u_at1(a.U, a.T, e, e)) - 2.0 * u_at1(a.U, a.T, i, e));
+        kbuf[e] = key;
     }
     __syncthreads();
+    const uint64_t key = kbuf[e];
+    int cnt = 0;
+#pragma unroll
+    for (int j0 = 0; j0 < 64; j0 += 8) {
+        uint64_t o[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = kbuf[64 * h + j0 + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = 64 * h + j0 + u;
+            cnt += (o[u] < key) || (o[u] == key && j < e);
+        }
+    }
+    if (h == 1) rk[e] = cnt;
+    __syncthreads();
+    if (h == 0) sbuf[cnt + rk[e]] = dkey_inv(key);
+    __syncthreads();
+    double acc = 0.0;
+    if (1 + tid <= k && 1 + tid < 128) acc += sbuf[1 + tid];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) red[wave] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        double sum = 0.0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) sum += red[w];
+        st1(a.scores + i, k > 0 ? sum : 0.0);
+        st1(a.diag + i, di);
+    }
+}
+
+// the last S item: rank, compact, margin (n <= 128, one workgroup).  Thread
+// t < n ranks row t against every key in LDS (broadcast reads); waves 0-1
+// compact the mask with ballots
+__device__ __forceinline__ void small_select(const SmallArgs &a, int wave, int lane,
+                                             uint64_t *keys, double *bnd, double *dg,
+                                             uint64_t *maskw) {
+    const int n = a.n, m = n - a.f;
+    const int tid = threadIdx.x;
+    double si = 0.0;
+    if (tid < n) {  // every score and diagonal in flight at once, into LDS
+        si = ld1(a.scores + tid);
+        keys[tid] = dkey(si);
+        dg[tid] = ld1(a.diag + tid);
+    }
+    __syncthreads();
+    bool on = false;
+    if (tid < n) {
+        const uint64_t ki = keys[tid];
+        int cnt = 0;
+        int j = 0;
+        for (; j + 8 <= n; j += 8) {
+            uint64_t o[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) o[u] = keys[j + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cnt += (o[u] < ki) || (o[u] == ki && j + u < tid);
+        }
+        for (; j < n; ++j) {
+            const uint64_t o = keys[j];
+            cnt += (o < ki) || (o == ki && j < tid);
+        }
+        on = cnt < m;
+        if (cnt == m - 1) bnd[0] = si;
+        if (cnt == m) bnd[1] = si;
+    }
+    if (tid < 3) maskw[tid] = 0;
+    __syncthreads();
+    if (on) atomicOr(reinterpret_cast<unsigned long long *>(&maskw[tid / 63]), 1ull << (tid % 63));
+    __syncthreads();
+    // compaction: rows 0..63 in wave 0, 64..127 in wave 1
+    __shared__ int wcount;
+    if (wave < 2) {
+        const uint64_t bal = __ballot(on);
+        if (wave == 0 && lane == 0) wcount = __popcll(bal);
+        __syncthreads();
+        const int pos = (wave ? wcount : 0) + __popcll(bal & ((1ull << lane) - 1));
+        if (on) st1(a.sel + pos, (int64_t)tid);
+    } else {
+        __syncthreads();
+    }
     if (wave == 0) {
-        int base = 0;
         double M = 0.0;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int j = lane + 64 * q;
-            const bool on = j < n && msk[j];
-            const uint64_t bal = __ballot(on);
-            const int pos = base + __popcll(bal & ((1ull << lane) - 1));
-            if (on) a.sel[pos] = j;
-            base += __popcll(bal);
             if (j < n) {
-                const double v = a.diag[j];
+                const double v = dg[j];
                 if (v == v && v < __builtin_inf() && v > M) M = v;
             }
         }
@@ -344,98 +469,162 @@ __device__ __forceinline__ void small_select(const SmallArgs &a, int wave, int l
 // M item c: mean of columns [256 c, 256 c + 256): each thread one column, the
 // m selected rows in ascending order (K4's order: the same bits)
 template <typename T>
-__device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int tid, int64_t *soff) {
+__device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int tid, int64_t *soff,
+                                           const uint64_t *maskw) {
     const int m = a.n - a.f;
-    for (int r = tid; r < m; r += 256) soff[r] = a.sel[r] * a.ld;
+    if (__popcll(maskw[0]) + __popcll(maskw[1]) + __popcll(maskw[2]) != m) {
+        // never index X with a damaged mask: report (BK_EHIP) and skip
+        if (tid == 0)
+            __hip_atomic_fetch_or(cline(a.ctr, C_ERR), 2u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (tid < a.n) {  // ascending selected rows from the mask the flag carried
+        const int w = tid / 63, b = tid % 63;
+        if ((maskw[w] >> b) & 1) {
+            int pos = __popcll(maskw[w] & ((1ull << b) - 1));
+            for (int u = 0; u < w; ++u) pos += __popcll(maskw[u]);
+            soff[pos] = (int64_t)tid * a.ld;
+        }
+    }
     __syncthreads();
     const int64_t col = (int64_t)c * 256 + tid;
     if (col < a.d) {
         const T *X = (const T *)a.X;
         double acc = 0.0;
         int r = 0;
-        for (; r + 16 <= m; r += 16) {
-            double v[16];
+        for (; r + 64 <= m; r += 64) {  // 64 loads in flight per thread
+            double v[64];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = (double)X[soff[r + u] + col];
+            for (int u = 0; u < 64; ++u) v[u] = (double)X[soff[r + u] + col];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) acc += v[u];
+            for (int u = 0; u < 64; ++u) acc += v[u];
+        }
+        if (r < m) {  // the rest, also in flight together
+            double v[64];
+#pragma unroll
+            for (int u = 0; u < 64; ++u) v[u] = r + u < m ? (double)X[soff[r + u] + col] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 64; ++u)
+                if (r + u < m) acc += v[u];
+            r = m;
         }
         for (; r < m; ++r) acc += (double)X[soff[r] + col];
         a.mean[col] = acc / (double)m;
     }
 }
 
-template <typename T, int NB>
+template <typename T>
+__device__ __forceinline__ void small_prefetch(const SmallArgs &a, int c, int tid) {
+    const int64_t col = (int64_t)c * 256 + tid;
+    if (col >= a.d) return;
+    const T *X = (const T *)a.X;
+    T acc = 0;
+    for (int r = 0; r < a.n; r += 16) {
+        T v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = r + u < a.n ? X[(int64_t)(r + u) * a.ld + col] : (T)0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += v[u];
+    }
+    asm volatile("" ::"v"(acc));  // keep the loads
+}
+
+template <typename T, bool VEC, int NB>
 __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     __shared__ int s_item;
     __shared__ unsigned s_old;
-    __shared__ __attribute__((aligned(16))) double kbuf[4][128];  // S: one row per wave
-    __shared__ double red[4][64];                                 // R: the 4 chains
-    __shared__ int msk[128];
+    __shared__ __attribute__((aligned(16))) char tile[16 * NB * SMALL_GR * 16];  // G: rows x KC columns
+    __shared__ uint64_t kbuf[128];                                      // S / selection keys
+    __shared__ __attribute__((aligned(16))) double sbuf[128];          // S: the sorted row
+    __shared__ int rk[128];
+    __shared__ double red[4][64];                                       // R chains, S waves
     __shared__ double bnd[2];
+    __shared__ double dgl[128];
     __shared__ int64_t soff[128];
+    __shared__ uint64_t maskw[3];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int total = a.P + a.Q + a.nS + a.C;
+    const int total = a.P + a.Q + a.n + a.C;
     unsigned *ctr = a.ctr;
     for (;;) {
         if (tid == 0)
-            s_item = (int)__hip_atomic_fetch_add(&ctr[C_HEAD], 1u, __ATOMIC_RELAXED,
+            s_item = (int)__hip_atomic_fetch_add(cline(ctr, C_HEAD), 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         const int it = s_item;
         __syncthreads();
         if (it >= total) break;
+        long long t0 = 0, m0 = 0;
+        if (a.trace && tid == 0) {
+            t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            m0 = (long long)__builtin_amdgcn_s_memtime();
+        }
         if (it < a.P) {
-            small_gram<T, NB>(a, it, wave, lane);
-            wg_signal(&ctr[C_G], &s_old);
+            small_gram<T, VEC, NB>(a, it, wave, lane, tile);
+            if (wg_arrive(ctr, C_G, (unsigned)a.P, &s_old)) wg_raise(ctr, F_G);
         } else if (it < a.P + a.Q) {
-            wg_wait(&ctr[C_G], (unsigned)a.P, &ctr[C_ERR]);
+            wg_wait_flag(ctr, F_G);
+            if (a.trace && tid == 0) a.trace[6 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
             small_reduce(a, it - a.P, tid, NB, red);
-            wg_signal(&ctr[C_R], &s_old);
-        } else if (it < a.P + a.Q + a.nS) {
-            wg_wait(&ctr[C_R], (unsigned)a.Q, &ctr[C_ERR]);
-            small_scores(a, it - a.P - a.Q, wave, lane, kbuf[wave]);
-            if (wg_signal(&ctr[C_S], &s_old) == (unsigned)a.nS - 1) {
-                // the last S item: every score and diagonal is published
-                if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                small_select(a, wave, lane, msk, bnd);
-                wg_signal(&ctr[C_SEL], &s_old);
+            if (wg_arrive(ctr, C_R, (unsigned)a.Q, &s_old)) wg_raise(ctr, F_R);
+        } else if (it < a.P + a.Q + a.n) {
+            wg_wait_flag(ctr, F_R);
+            if (a.trace && tid == 0) a.trace[6 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+            small_scores(a, it - a.P - a.Q, tid, kbuf, sbuf, rk, &red[0][0]);
+            if (wg_arrive(ctr, C_S, (unsigned)a.n, &s_old)) {
+                // the last S item: every score and diagonal is published;
+                // small_select reads them sc1
+                small_select(a, wave, lane, kbuf, bnd, dgl, maskw);
+                uint64_t w3[3] = {maskw[0], maskw[1], maskw[2]};
+                sel_raise(ctr, w3);
             }
         } else {
-            wg_wait(&ctr[C_SEL], 1u, &ctr[C_ERR]);
-            small_mean<T>(a, it - a.P - a.Q - a.nS, tid, soff);
+            // while the selection is computed: pull this item's columns of
+            // every row toward this XCD's L2, so the mean's loads hit it
+            small_prefetch<T>(a, it - a.P - a.Q - a.n, tid);
+            sel_wait(ctr, maskw);
+            if (a.trace && tid == 0) a.trace[6 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+            small_mean<T>(a, it - a.P - a.Q - a.n, tid, soff, maskw);
+        }
+        if (a.trace && tid == 0) {
+            unsigned hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            a.trace[6 * it] = t0;
+            a.trace[6 * it + 2] = (long long)__builtin_amdgcn_s_memrealtime();
+            a.trace[6 * it + 3] = (long long)hw | ((long long)blockIdx.x << 32);
+            a.trace[6 * it + 4] = m0;
+            a.trace[6 * it + 5] = (long long)__builtin_amdgcn_s_memtime();
         }
     }
     // the last workgroup out resets the queue for the next launch (stream
-    // order: the next launch starts after this one has completed)
-    if (tid == 0) {
-        const unsigned e = __hip_atomic_fetch_add(&ctr[C_EXIT], 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        if (e == gridDim.x - 1) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            if (ctr_load(&ctr[C_ERR])) {  // a wait gave up: the outputs are invalid
-                a.margin[0] = __builtin_nan("");
-                a.margin[2] = 2.0;  // read_margin reports BK_EHIP
-            }
-            for (int c = C_HEAD; c <= C_ERR; ++c)
-                __hip_atomic_store(&ctr[c], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // order: the next launch starts after this one has completed) -- every
+    // word of every line: the F_SEL lines carry the mask in words 0..5
+    if (tid == 0)
+        s_old = __hip_atomic_fetch_add(cline(ctr, C_EXIT), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_old == gridDim.x - 1) {
+        if (tid == 0 && ctr_load(cline(ctr, C_ERR))) {  // a wait gave up: outputs invalid
+            a.margin[0] = __builtin_nan("");
+            a.margin[2] = 2.0;  // read_margin reports BK_EHIP
         }
+        __syncthreads();
+        for (int w = tid; w < C_LINES * 32; w += 256)
+            __hip_atomic_store(ctr + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-template <typename T>
+template <typename T, bool VEC>
 static void launch_small_t(const SmallArgs &a, int NBv, int grid, hipStream_t st) {
     switch (NBv) {
-    case 1: hipLaunchKernelGGL((k_small<T, 1>), dim3(grid), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((k_small<T, 2>), dim3(grid), dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((k_small<T, 3>), dim3(grid), dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((k_small<T, 4>), dim3(grid), dim3(256), 0, st, a); break;
-    case 5: hipLaunchKernelGGL((k_small<T, 5>), dim3(grid), dim3(256), 0, st, a); break;
-    case 6: hipLaunchKernelGGL((k_small<T, 6>), dim3(grid), dim3(256), 0, st, a); break;
-    case 7: hipLaunchKernelGGL((k_small<T, 7>), dim3(grid), dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_small<T, 8>), dim3(grid), dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((k_small<T, VEC, 1>), dim3(grid), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_small<T, VEC, 2>), dim3(grid), dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((k_small<T, VEC, 3>), dim3(grid), dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_small<T, VEC, 4>), dim3(grid), dim3(256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((k_small<T, VEC, 5>), dim3(grid), dim3(256), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((k_small<T, VEC, 6>), dim3(grid), dim3(256), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((k_small<T, VEC, 7>), dim3(grid), dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_small<T, VEC, 8>), dim3(grid), dim3(256), 0, st, a); break;
     }
 }
 
@@ -443,16 +632,12 @@ SmallPlan small_plan(int n, int64_t d, int num_cu) {
     SmallPlan p;
     p.nb16 = (n + 15) / 16;
     p.nblk = p.nb16 * (p.nb16 + 1) / 2;
-    int64_t kc = 64;
-    if (const char *e = getenv("BK_SMALL_KC")) kc = atoll(e) > 0 ? atoll(e) : kc;
-    kc = (kc + 7) / 8 * 8;
-    // at most 2 partial rounds per CU: the R items read P partials each
-    const int64_t pmax = 2 * (int64_t)num_cu;
-    if ((d + kc - 1) / kc > pmax) kc = ((d + pmax - 1) / pmax + 7) / 8 * 8;
+    (void)num_cu;
+    const int64_t kc = SMALL_KC;
     p.kc = (int)kc;
     p.P = (int)((d + kc - 1) / kc);
     p.Q = 4 * p.nblk;
-    p.nS = (n + 3) / 4;
+    p.nS = n;  // one S item per row
     p.C = (int)((d + 255) / 256);
     return p;
 }
@@ -460,8 +645,9 @@ SmallPlan small_plan(int n, int64_t d, int num_cu) {
 hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
-                        hipStream_t st) {
+                        hipStream_t st, long long *trace) {
     SmallArgs a;
+    a.trace = trace;
     a.X = X;
     a.ld = ld;
     a.d = d;
@@ -482,12 +668,17 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     a.margin = margin;
     a.sel = sel;
     a.ctr = ctr;
-    const int total = a.P + a.Q + a.nS + a.C;
+    const int total = a.P + a.Q + a.n + a.C;
     const int grid = total < num_cu ? total : num_cu;
-    if (dtype == 0)
-        launch_small_t<double>(a, p.nb16, grid, st);
+    const bool vec = (ld % 2) == 0 && ((uintptr_t)X % (dtype == 0 ? 16 : 8)) == 0;
+    if (dtype == 0 && vec)
+        launch_small_t<double, true>(a, p.nb16, grid, st);
+    else if (dtype == 0)
+        launch_small_t<double, false>(a, p.nb16, grid, st);
+    else if (vec)
+        launch_small_t<float, true>(a, p.nb16, grid, st);
     else
-        launch_small_t<float>(a, p.nb16, grid, st);
+        launch_small_t<float, false>(a, p.nb16, grid, st);
     return hipGetLastError();
 }
 

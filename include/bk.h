@@ -97,8 +97,8 @@ int bk_multikrum(bk_ctx *ctx, const void *X, int where, int dtype, int64_t n, in
 int bk_multikrum_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
                         int64_t ld, int64_t f, int64_t *d_sel_idx, double *d_scores,
                         double *d_mean);
-/* Small batches (n <= 128, d <= 262144, rows aligned for 16-B fp64 / 8-B fp32
- * loads: Biscotti's deployed shapes, configs A and B) run as ONE launch,
+/* Small batches (n <= 128, d <= 32768: Biscotti's deployed shapes, configs A
+ * and B) run as ONE launch,
  * k_small: split-K Gram, reduce, scores, selection and mean pulled as work
  * items from a queue in dependency order (no co-residency assumed).  The same
  * results as the general path: selection, and the mean bitwise; scores within
