@@ -16,7 +16,7 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
-BK_ABI_VERSION = 7
+BK_ABI_VERSION = 8
 BK_F32_EXACT, BK_F32_MFMA, BK_F32_CERTIFIED = 0, 1, 2
 KERNELS = ["k_gram", "k_reduce", "k_transpose", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni",
@@ -57,6 +57,7 @@ SIGNATURES = {
     "bk_graph_enable": (_i, [_p, _i]),
     "bk_set_f32_mode": (_i, [_p, _i]),
     "bk_timing_select": (_i, [_p, ctypes.c_uint32]),
+    "bk_timing_stride": (_i, [_p, ctypes.c_int]),
     "bk_timing_read": (_i, [_p, _i, _pd, _pi64]),
     "bk_kernel_name": (ctypes.c_char_p, [_i]),
     "bk_plan": (_i, [_p, _i64, _i64, _pi64, _pi64, _pi64, _pi64]),

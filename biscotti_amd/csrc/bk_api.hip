@@ -101,6 +101,8 @@ struct bk_ctx {
     std::vector<void *> staged;
     // timing
     uint32_t timing = 0;  // bit k: record HIP events around kernel k (bk_timing_select)
+    int tstride = 1;      // ... on every tstride-th launch of it (bk_timing_stride)
+    int64_t tseq[BK_NUM_KERNELS] = {0};
     struct Ev {
         int kid;
         hipEvent_t a, b;
@@ -192,7 +194,10 @@ int get_event(bk_ctx *c, hipEvent_t *out) {
 }
 
 // Bracket one launch with events when timing is on.
-bool timing_on(const bk_ctx *c, int kid) { return (c->timing >> kid) & 1u; }
+bool timing_on(bk_ctx *c, int kid) {
+    if (!((c->timing >> kid) & 1u)) return false;
+    return c->tstride <= 1 || (c->tseq[kid]++ % c->tstride) == 0;
+}
 
 template <typename F>
 int timed(bk_ctx *c, int kid, F &&launch) {
@@ -432,8 +437,9 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
 // launch beats the chain
 bool small_ok(const bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld) {
     static const int64_t dmax = [] {
-        const char *e = getenv("BK_SMALL_MAX_D");
-        return e ? atoll(e) : (int64_t)32768;  // P = d / 64 partials: <= 4 load rounds in R
+        const char *e = getenv("BK_SMALL_MAX_D");  // may only lower the cap
+        const int64_t v = e ? atoll(e) : (int64_t)32768;
+        return v < 32768 ? v : (int64_t)32768;  // d / 64 chunks: <= 1024 G items (k_small's groups)
     }();
     (void)dX;
     (void)dtype;
@@ -458,11 +464,11 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
         sc = (double *)c->scores.p;
     }
     long long *trace = nullptr;
-    const int items = sp.P + sp.Q + sp.nS + (d_mean ? sp.C : 0);
+    const int items = sp.ng + sp.Q + sp.nS + (d_mean ? sp.C : 1);
     const char *tfile = getenv("BK_SMALL_TRACE");  // debug: per-item timeline
     if (tfile) {
-        CHK(ensure(c->trace, (size_t)items * 6 * sizeof(long long)));
-        HIPCHK(hipMemsetAsync(c->trace.p, 0, (size_t)items * 6 * sizeof(long long), c->stream));
+        CHK(ensure(c->trace, (size_t)items * 8 * sizeof(long long)));
+        HIPCHK(hipMemsetAsync(c->trace.p, 0, (size_t)items * 8 * sizeof(long long), c->stream));
         trace = (long long *)c->trace.p;
     }
     CHK(timed(c, BK_K_SMALL, [&] {
@@ -473,13 +479,13 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
     }));
     c->margin_valid = 1;
     if (tfile) {
-        std::vector<long long> h((size_t)items * 6 + 5);
+        std::vector<long long> h((size_t)items * 8 + 5);
         h[0] = items;
-        h[1] = sp.P;
+        h[1] = sp.ng;  // G items
         h[2] = sp.Q;
         h[3] = sp.nS;
-        h[4] = d_mean ? sp.C : 0;
-        HIPCHK(hipMemcpyAsync(h.data() + 5, trace, (size_t)items * 6 * sizeof(long long),
+        h[4] = d_mean ? sp.C : 1;
+        HIPCHK(hipMemcpyAsync(h.data() + 5, trace, (size_t)items * 8 * sizeof(long long),
                               hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (FILE *fp = fopen(tfile, "ab")) {
@@ -1091,7 +1097,8 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
     }
     if (c->comm) {  // also at 1 rank, so the exchange is exercised on a 1-GPU box
         hipEvent_t a = nullptr, b = nullptr;
-        if (timing_on(c, BK_K_ALLREDUCE)) {
+        const bool ton = timing_on(c, BK_K_ALLREDUCE);
+        if (ton) {
             CHK(get_event(c, &a));
             CHK(get_event(c, &b));
             HIPCHK(hipEventRecord(a, c->stream));
@@ -1104,7 +1111,7 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
             RCCLCHK(ncclAllGather(U, Ug, (size_t)usz, ncclDouble, c->comm, c->stream));
             HIPCHK(launch_sum_ranks(Ug, c->nranks, usz, U, c->stream));
         }
-        if (timing_on(c, BK_K_ALLREDUCE)) {
+        if (ton) {
             HIPCHK(hipEventRecord(b, c->stream));
             c->pending.push_back({BK_K_ALLREDUCE, a, b});
         }
@@ -1509,6 +1516,14 @@ int bk_timing_enable(bk_ctx *c, int on) {
     return bk_timing_select(c, on ? ~0u : 0u);
 }
 
+int bk_timing_stride(bk_ctx *c, int every) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    if (every < 1) return fail(BK_EINVAL, "timing stride %d < 1", every);
+    const uint32_t mask = c->timing;
+    c->tstride = every;
+    return bk_timing_select(c, mask);  // clears, keeps the selection
+}
+
 int bk_timing_select(bk_ctx *c, uint32_t mask) {
     if (!c) return fail(BK_EINVAL, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1522,6 +1537,7 @@ int bk_timing_select(bk_ctx *c, uint32_t mask) {
     for (int i = 0; i < BK_NUM_KERNELS; ++i) {
         c->tot_ms[i] = 0;
         c->cnt[i] = 0;
+        c->tseq[i] = 0;
     }
     c->timing = mask;
     return BK_OK;

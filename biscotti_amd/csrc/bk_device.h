@@ -42,6 +42,7 @@ struct K2Ord<uint64_t> {
     static __device__ __forceinline__ uint64_t bits(uint64_t a) { return a; }
     static __device__ __forceinline__ uint64_t from(uint64_t b) { return b; }
     static __device__ __forceinline__ double val(uint64_t a) { return dkey_inv(a); }
+    static __device__ __forceinline__ uint64_t neg(uint64_t a) { return ~a; }  // order-reversing
 };
 template <>
 struct K2Ord<double> {  // no NaN in the row: IEEE min / max
@@ -50,6 +51,7 @@ struct K2Ord<double> {  // no NaN in the row: IEEE min / max
     static __device__ __forceinline__ uint64_t bits(double a) { return (uint64_t)__double_as_longlong(a); }
     static __device__ __forceinline__ double from(uint64_t b) { return __longlong_as_double((long long)b); }
     static __device__ __forceinline__ double val(double a) { return a; }
+    static __device__ __forceinline__ double neg(double a) { return -a; }  // order-reversing
 };
 
 template <typename K>

@@ -117,10 +117,10 @@ hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, con
                        unsigned int *cnt, double *scores, hipStream_t st);
 // bk_small.hip: the whole Multi-Krum of a small batch (n <= 128) in one launch
 struct SmallPlan {
-    int nb16 = 0, nblk = 0, kc = 0, P = 0, Q = 0, nS = 0, C = 0;
+    int nb16 = 0, nblk = 0, kc = 0, P = 0, ng = 0, Q = 0, nS = 0, C = 0;  // P chunks, ng G items
 };
 SmallPlan small_plan(int n, int64_t d, int num_cu);
-constexpr int SMALL_CTR_WORDS = 30 * 32;  // 30 queue lines of 128 B (bk_small.hip)
+constexpr int SMALL_CTR_WORDS = 71 * 32;  // 71 queue lines of 128 B (bk_small.hip)
 hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,

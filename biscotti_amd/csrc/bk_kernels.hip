@@ -1109,15 +1109,160 @@ __device__ __forceinline__ void k2_sort(K (&v)[KPT], K *keys_lds, int N, int tid
     __syncthreads();
 }
 
+// K2 v3 sort, 16 keys per thread (N >= 4096): every compare-exchange inside a
+// thread.  A stage on index bit b is register-local when b is one of the 4
+// bits the current layout keeps in the register index; layout L_j keeps bits
+// j .. j+3 there (thread t, register q hold key e = (t mod 2^j) | q 2^j |
+// (t >> j) 2^(j+4)), and a merge of 2^B keys walks its bits B-1 .. 0 in
+// chunks of 4, moving the keys to L_(hi-3) .. L_0 through LDS before each
+// chunk (3 moves per merge at N = 4096, 20 in all) instead of lane exchanges
+// (v2: 33 DPP / swizzle / bpermute stages of ~6 instructions per key).  The
+// merges use the classic alternating directions, folded into the keys:
+// before merge B the keys of blocks with bit B set are negated (order
+// reversed: -x for fp64, ~x for the u64 keys), so every stage keeps the
+// minimum at the lower index and the sequence entering each merge is bitonic;
+// at B = log2 N nothing is negated.  LDS words are padded by one per 16 keys
+// (word e + e/16), which keeps every layout's 16-lane write groups and 32-lane
+// read groups on distinct banks.  Any correct sort gives the same array.
+__device__ __forceinline__ int k2_pad(int e) { return e + (e >> 4); }
+template <int J>
+__device__ __forceinline__ int k2_lbase(int t) {
+    const int e = (t & ((1 << J) - 1)) | ((t >> J) << (J + 4));
+    return e + (e >> 4);
+}
+template <int J>
+__device__ __forceinline__ constexpr int k2_loff(int q) {  // padded word of (t, q) - of (t, 0)
+    if constexpr (J >= 4)
+        return (q << J) + (q << (J - 4));
+    else
+        return (q << J) + (q >> (4 - J));
+}
+template <typename K, int J>
+__device__ __forceinline__ void k2_put(const K (&v)[16], K *lds, int t) {
+    K *p = lds + k2_lbase<J>(t);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) p[k2_loff<J>(q)] = v[q];
+}
+template <typename K, int J>
+__device__ __forceinline__ void k2_get(K (&v)[16], const K *lds, int t) {
+    const K *p = lds + k2_lbase<J>(t);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = p[k2_loff<J>(q)];
+}
+// the ordering point of a move: a workgroup barrier, or -- when every key
+// stays inside its wave -- only a compiler fence (a wave's LDS operations
+// execute in order, so its reads see its own lanes' writes)
+__device__ __forceinline__ void k2_sync(bool local) {
+    if (local) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+// L_from -> L_to.  Thread bits 6.. (the wave index) are key bits 10.. in every
+// layout L_j with j <= 6, so a move between two such layouts keeps each key in
+// its wave, in the wave's own LDS words: no workgroup barrier (16 of the 20
+// moves at N = 4096)
+template <typename K>
+__device__ __forceinline__ void k2_move(K (&v)[16], K *lds, int t, int from, int to) {
+    const bool local = from <= 6 && to <= 6;
+    k2_sync(local);  // earlier readers of these words are done
+    switch (from) {
+    case 0: k2_put<K, 0>(v, lds, t); break;
+    case 1: k2_put<K, 1>(v, lds, t); break;
+    case 2: k2_put<K, 2>(v, lds, t); break;
+    case 3: k2_put<K, 3>(v, lds, t); break;
+    case 4: k2_put<K, 4>(v, lds, t); break;
+    case 5: k2_put<K, 5>(v, lds, t); break;
+    case 6: k2_put<K, 6>(v, lds, t); break;
+    case 7: k2_put<K, 7>(v, lds, t); break;
+    case 8: k2_put<K, 8>(v, lds, t); break;
+    case 9: k2_put<K, 9>(v, lds, t); break;
+    default: k2_put<K, 10>(v, lds, t); break;
+    }
+    k2_sync(local);
+    switch (to) {
+    case 0: k2_get<K, 0>(v, lds, t); break;
+    case 1: k2_get<K, 1>(v, lds, t); break;
+    case 2: k2_get<K, 2>(v, lds, t); break;
+    case 3: k2_get<K, 3>(v, lds, t); break;
+    case 4: k2_get<K, 4>(v, lds, t); break;
+    case 5: k2_get<K, 5>(v, lds, t); break;
+    case 6: k2_get<K, 6>(v, lds, t); break;
+    case 7: k2_get<K, 7>(v, lds, t); break;
+    case 8: k2_get<K, 8>(v, lds, t); break;
+    case 9: k2_get<K, 9>(v, lds, t); break;
+    default: k2_get<K, 10>(v, lds, t); break;
+    }
+}
+// an ascending stage on register bit R (pairs q, q + 2^R)
+template <typename K, int R>
+__device__ __forceinline__ void k2_rstage(K (&v)[16]) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+        if (!(q & (1 << R))) k2_cas(v[q], v[q | (1 << R)]);
+}
+template <typename K>
+__device__ __forceinline__ void k2_rstages(K (&v)[16], int top) {  // register bits top .. 0
+    switch (top) {
+    case 3: k2_rstage<K, 3>(v); [[fallthrough]];
+    case 2: k2_rstage<K, 2>(v); [[fallthrough]];
+    case 1: k2_rstage<K, 1>(v); [[fallthrough]];
+    default: k2_rstage<K, 0>(v);
+    }
+}
+template <typename K>
+__device__ __forceinline__ void k2_negate(K (&v)[16]) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = K2Ord<K>::neg(v[q]);
+}
+// v: thread t's keys t*16 .. t*16+15 (L_0); on return the whole row sorted
+// ascending sits in lds at the padded words k2_pad(e)
+template <typename K>
+__device__ __forceinline__ void k2_sort16(K (&v)[16], K *lds, int N, int tid) {
+    if (tid & 1) k2_negate(v);  // blocks of 16 with bit 4 set sort descending
+    // merges of 2 .. 16 keys inside the thread (all-ascending mirror form)
+#pragma unroll
+    for (int size = 2; size <= 16; size <<= 1) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int p = q ^ (size - 1);
+            if (q < p && ((q ^ p) & (size >> 1))) k2_cas(v[q], v[p]);
+        }
+#pragma unroll
+        for (int st = size >> 2; st >= 1; st >>= 1)
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if ((q & st) == 0) k2_cas(v[q], v[q + st]);
+    }
+    for (int B = 5; (1 << B) <= N; ++B) {
+        if (((tid >> (B - 4)) ^ (tid >> (B - 5))) & 1) k2_negate(v);  // direction of merge B
+        int cur = 0;
+        for (int hi = B - 1; hi >= 0;) {
+            const int j = hi > 3 ? hi - 3 : 0;
+            k2_move(v, lds, tid, cur, j);
+            cur = j;
+            k2_rstages(v, hi - j);
+            hi = j - 1;
+        }
+    }
+    __syncthreads();
+    k2_put<K, 0>(v, lds, tid);
+    __syncthreads();
+}
+
 // v1's summation shape over the sorted keys (virtual thread t' = tid + NT h)
-template <typename K, int NT, int NT_SUM>
+template <typename K, int NT, int NT_SUM, bool PAD = false>
 __device__ __forceinline__ double k2_sum(const K *keys_lds, int64_t k, int tid, double *red) {
     constexpr int H = NT_SUM / NT;
     const int lane = tid & 63;
 #pragma unroll
     for (int h = 0; h < H; ++h) {
         double acc = 0.0;
-        for (int64_t r = 1 + tid + NT * h; r <= k; r += NT_SUM) acc += K2Ord<K>::val(keys_lds[r]);
+        for (int64_t r = 1 + tid + NT * h; r <= k; r += NT_SUM)
+            acc += K2Ord<K>::val(keys_lds[PAD ? k2_pad((int)r) : r]);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if (lane == 0) red[(tid >> 6) + (NT / 64) * h] = acc;
@@ -1159,6 +1304,7 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
     if (tid == 0) diag[i] = di;
     // distances, element e = tid + NT q (consecutive lanes, consecutive
     // columns: coalesced row reads), through LDS into the blocked layout
+    constexpr bool V3 = KPT == 16;  // the register-local sort (k2_sort16)
     double *kd = reinterpret_cast<double *>(keys);
     bool nan = false;
 #pragma unroll
@@ -1174,7 +1320,7 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
             x = x == 0.0 ? 0.0 : x;  // -0 == +0 (v1's dkey)
             nan |= x != x;
         }
-        kd[e] = x;
+        kd[V3 ? k2_pad(e) : e] = x;
     }
     if (MODE == 1) {
         if (kd[tid] == 1.2345) scores[i] = kd[tid];  // keep the loads
@@ -1182,19 +1328,33 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
     }
     __syncthreads();
     double dv[KPT];
+    if constexpr (V3) {
+        k2_get<double, 0>(dv, kd, tid);
+    } else {
 #pragma unroll
-    for (int q = 0; q < KPT; ++q) dv[q] = kd[tid * KPT + q];
+        for (int q = 0; q < KPT; ++q) dv[q] = kd[tid * KPT + q];
+    }
     double sum;
     if (!__syncthreads_or(nan)) {  // (the barrier also orders kd[] reads before the sort's writes)
-        k2_sort<double, NT, KPT>(dv, reinterpret_cast<double *>(keys), N, tid);
-        sum = k2_sum<double, NT, NT_SUM>(reinterpret_cast<const double *>(keys), k, tid, red);
+        if constexpr (V3) {
+            k2_sort16<double>(dv, kd, N, tid);
+            sum = k2_sum<double, NT, NT_SUM, true>(kd, k, tid, red);
+        } else {
+            k2_sort<double, NT, KPT>(dv, kd, N, tid);
+            sum = k2_sum<double, NT, NT_SUM>(kd, k, tid, red);
+        }
     } else {  // a NaN in the row: v1's order-preserving keys, NaN last
         uint64_t v[KPT];
 #pragma unroll
         for (int q = 0; q < KPT; ++q)
             v[q] = tid * KPT + q < n ? dkey(dv[q]) : ~0ULL;
-        k2_sort<uint64_t, NT, KPT>(v, keys, N, tid);
-        sum = k2_sum<uint64_t, NT, NT_SUM>(keys, k, tid, red);
+        if constexpr (V3) {
+            k2_sort16<uint64_t>(v, keys, N, tid);
+            sum = k2_sum<uint64_t, NT, NT_SUM, true>(keys, k, tid, red);
+        } else {
+            k2_sort<uint64_t, NT, KPT>(v, keys, N, tid);
+            sum = k2_sum<uint64_t, NT, NT_SUM>(keys, k, tid, red);
+        }
     }
     if (tid == 0) scores[i] = (k > 0) ? sum : 0.0;
 }
@@ -1488,7 +1648,7 @@ static void launch_scores2(const double *U, const double *Ut, const double *dg, 
         const char *e = getenv("BK_K2_MODE");  // timing-only ablations (tools/), never tests
         return e ? atoi(e) : 0;
     }();
-    const size_t lds = (size_t)N * sizeof(uint64_t);
+    const size_t lds = (size_t)(KPT == 16 ? N + N / 16 : N) * sizeof(uint64_t);  // v3: padded
     if (mode == 1)
         hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 1>), dim3(n), dim3(NT), lds, st, U, Ut,
                            dg, T, n, N, k, scores, diag);
@@ -1720,7 +1880,7 @@ hipError_t configure_kernels() {
                            (const void *)k_scores2<512, 16, 1024, true, 2>,
                            (const void *)k_scores2<1024, 16, 1024, true, 2>,
                            (const void *)k_scores2<1024, 4, 1024, true, 2>}) {
-        e = hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+        e = hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, 144 * 1024);  // v3 at N = 16384: 136 KiB
         if (e != hipSuccess) return e;
     }
     // the masked column sums keep up to BK_MAX_N row offsets in LDS

@@ -8,19 +8,23 @@
 // persistent launch whose workgroups pull ITEMS from a queue (one returning
 // atomic per item) in dependency order:
 //
-//   G items  (P of them)  split-K Gram partial of d/P columns: every upper
-//                          16x16 block of the (n <= 128) Gram, fp64 MFMA
+//   G items  (4 per 128    split-K Gram partial of 128 columns: a quarter of
+//             columns)     the upper 16x16 blocks of the (n <= 128) Gram
+//                          each, fp64 MFMA
 //   R items  (4 per block) fixed-order sum of the P partials -> packed upper U
 //   S items  (one per row) distances, sort by counting, sum of ranks 1..k in
-//                          K2's exact shape; the last S item to finish (its
-//                          arrival add returns n - 1) ranks the scores,
-//                          compacts the selection, writes the margin
-//   M items  (256 columns) mean of the selected rows, ascending (K4's order)
+//                          K2's exact shape
+//   M items  (128 columns) rank the n scores (each item itself: no serial
+//                          selection step), compact the selection, mean of
+//                          the selected rows ascending (K4's order); item 0
+//                          writes sel and the margin
 //
-// An item only waits (a relaxed sc1 poll of a counter) for items dequeued
-// BEFORE it, and a dequeued item's workgroup is running, so the queue always
-// drains: no co-residency is assumed (MI355X_MICROARCH.md, "Workgroup
-// dispatch").  Hand-offs are the guide's write-through form ("Valid forms",
+// The first G items go to workgroups 0.. by blockIdx, the rest are dequeued
+// in order.  An item only waits (a relaxed sc1 poll of a counter) for items
+// before it: dequeued ones run on running workgroups, and the statically held
+// G items wait for nothing, so their workgroups finish once dispatched.  No
+// co-residency is assumed, only that every workgroup of the grid (<= one per
+// CU) is eventually dispatched (MI355X_MICROARCH.md, "Workgroup dispatch").  Hand-offs are the guide's write-through form ("Valid forms",
 // table row 1): EVERY store of handed-off bytes is an sc1 store (agent-scope
 // relaxed atomic store), every storing wave drains vmcnt(0), a workgroup
 // barrier, then one lane's agent-scope atomic add; EVERY load of them is an
@@ -38,17 +42,39 @@
 
 namespace bk {
 
-// queue words, each on a 128-B line of its own: the item head, the arrival
-// counters of the G, R and S phases, the exit count, the error word; then the
-// "phase done" flags F_G, F_R, F_SEL, each replicated once per XCD (a waiting
-// workgroup polls its own XCD's copy: 1/8 of the pollers on any line)
-enum { C_HEAD = 0, C_G = 1, C_R = 2, C_S = 3, C_EXIT = 4, C_ERR = 5, F_G = 6, F_R = 14, F_SEL = 22,
-       C_LINES = 30 };
+// queue words, each on a 128-B line of its own: the item head, the top
+// arrival counters of the G, R and S phases, a spare line, the error word;
+// then the "phase done" flags F_G, F_R, F_S, each replicated once per XCD (a
+// waiting workgroup polls its own XCD's copy: 1/8 of the pollers on any
+// line); then the arrival counters of groups of 32 items (G_GRP: up to 1024 G
+// items, R_GRP: 144 R items, S_GRP: 128 S items).  Same-address atomics
+// serialize at ~11 ns each, so 246 G items arriving together on one counter
+// took ~2.7 us; a group's last arriver (told by its add's return value) adds
+// once to the phase's top counter instead.
+enum { C_HEAD = 0, C_G = 1, C_R = 2, C_S = 3, C_SPARE = 4, C_ERR = 5, F_G = 6, F_R = 14, F_S = 22,
+       G_GRP = 30, R_GRP = 62, S_GRP = 67, C_LINES = 71 };
+static_assert(C_LINES * 32 == SMALL_CTR_WORDS, "bk_internal.h SMALL_CTR_WORDS");
 #ifndef BK_SMALL_KC
-#define BK_SMALL_KC 64
+#define BK_SMALL_KC 128
 #endif
-constexpr int SMALL_KC = BK_SMALL_KC;  // columns per G item (groups of 8)
+constexpr int SMALL_KC = BK_SMALL_KC;  // columns per chunk (groups of 8)
 constexpr int SMALL_GR = SMALL_KC / 2;  // 16-B granules per staged row
+constexpr int SMALL_SPLIT = 4;          // G items per chunk (each: a quarter of the blocks)
+
+// G item it -> (chunk c, part h).  The SPLIT parts of a chunk are items 8
+// apart, so under the static first assignment (workgroup b runs item b;
+// blocks b, b + 8 share an XCD) they stage the same columns through one L2
+__device__ __forceinline__ void g_item(int it, int P, int &c, int &h) {
+    const int full = (P >> 3) * (8 * SMALL_SPLIT);
+    if (it < full) {
+        h = (it >> 3) % SMALL_SPLIT;
+        c = 8 * (it / (8 * SMALL_SPLIT)) + (it & 7);
+    } else {
+        const int t = it - full, r = P & 7;
+        h = t / r;
+        c = (P & ~7) + t % r;
+    }
+}
 
 struct SmallArgs {
     const void *X;
@@ -58,7 +84,7 @@ struct SmallArgs {
     int64_t *sel;
     unsigned *ctr;
     long long *trace;  // debug (BK_SMALL_TRACE): per item {start, waited, end, hw id,
-                       // shader clock at start, at end}
+                       // shader clock at start, at end, two in-item stamps}
 };
 
 __device__ __forceinline__ unsigned ctr_load(const unsigned *p) {
@@ -82,6 +108,11 @@ __device__ __forceinline__ double u_at1(const double *U, int T, int r, int c) {
 }
 
 __device__ __forceinline__ unsigned *cline(unsigned *ctr, int line) { return ctr + 32 * line; }
+
+// debug trace: in-item stamp q (0, 1) of the current item (tr = its record)
+__device__ __forceinline__ void stamp(long long *tr, int q) {
+    if (tr && threadIdx.x == 0) tr[6 + q] = (long long)__builtin_amdgcn_s_memrealtime();
+}
 
 __device__ __forceinline__ int xcc_id() {
     unsigned x;
@@ -107,18 +138,28 @@ __device__ __forceinline__ void wg_wait_flag(unsigned *ctr, int flag) {
     __syncthreads();
 }
 
-// every wave drains its sc1 stores, then one lane counts the arrival; the
-// workgroup whose add returns last - 1 sees every other producer's bytes
-// (the guide's row 1: the last adder, told by the value its add returned)
-__device__ __forceinline__ bool wg_arrive(unsigned *ctr, int counter, unsigned last,
-                                          unsigned *s_old) {
+// every wave drains its sc1 stores, then one lane counts the arrival of item
+// idx (of count) on its group's counter; the group's last arriver counts the
+// group on the phase's top counter, and the workgroup whose top add returns
+// ngroups - 1 sees every other producer's bytes (the guide's row 1: the last
+// adder, told by the value its add returned; each group's last adder saw its
+// members' adds, which followed their drained sc1 stores)
+__device__ __forceinline__ bool wg_arrive(unsigned *ctr, int top, int grp, int idx, int count,
+                                          unsigned *s_last) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
-        *s_old = __hip_atomic_fetch_add(cline(ctr, counter), 1u, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        const int g = idx >> 5, gs = count - 32 * g < 32 ? count - 32 * g : 32;
+        const unsigned ng = (unsigned)((count + 31) >> 5);
+        unsigned last = 0;
+        if (__hip_atomic_fetch_add(cline(ctr, grp + g), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == (unsigned)gs - 1u)
+            last = __hip_atomic_fetch_add(cline(ctr, top), 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) == ng - 1u;
+        *s_last = last;
+    }
     __syncthreads();
-    return *s_old == last - 1;
+    return *s_last != 0;
 }
 
 // the last arriver raises a phase flag on every XCD's copy (one wave
@@ -127,36 +168,6 @@ __device__ __forceinline__ void wg_raise(unsigned *ctr, int flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < 8) st1(cline(ctr, flag + (int)threadIdx.x), 1u);
-}
-
-// F_SEL carries the selection itself: rows 63w .. 63w+62 in bits 0..62 of
-// u64 word w (w < 3) of every XCD's flag line, bit 63 set in each word; a
-// word is one 8-B sc1 store (single-copy atomic), and a reader that sees bit
-// 63 in all three has the whole mask -- no separate round trip for sel
-__device__ __forceinline__ void sel_raise(unsigned *ctr, const uint64_t (&w)[3]) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x < 24) {
-        uint64_t *line = reinterpret_cast<uint64_t *>(cline(ctr, F_SEL + (int)threadIdx.x / 3));
-        st1(line + threadIdx.x % 3, (uint64_t)(w[threadIdx.x % 3] | (1ull << 63)));
-    }
-}
-__device__ __forceinline__ void sel_wait(unsigned *ctr, uint64_t *mask_lds) {
-    if (threadIdx.x < 3) {
-        const uint64_t *line = reinterpret_cast<const uint64_t *>(cline(ctr, F_SEL + xcc_id()));
-        uint64_t v;
-        uint64_t spins = 0;
-        while (!((v = ld1(line + threadIdx.x)) >> 63)) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1ull << 24)) {
-                __hip_atomic_fetch_or(cline(ctr, C_ERR), 1u, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        mask_lds[threadIdx.x] = v & ~(1ull << 63);
-    }
-    __syncthreads();
 }
 
 // upper 16x16 block b (row-major over bi <= bj) of an NB x NB block grid
@@ -262,12 +273,13 @@ struct SmallStage {
     }
 };
 
-// the MFMAs of 8-column groups [t0, t1) of the staged tile
-template <int NB, int W, int NJ>
+// the MFMAs of 8-column groups [t0, t1) of the staged tile, blocks J0 .. J1-1
+// of this wave's list
+template <int NB, int W, int J0, int J1>
 __device__ __forceinline__ void small_gram_groups(d4 *acc, const char *tile, int lane, int t0,
                                                   int t1) {
     const int rr = lane & 15, g = lane >> 4;
-    if constexpr (NJ > 0) {
+    if constexpr (J1 > J0) {
 #pragma unroll
         for (int t = 0; t < SMALL_KC / 8; ++t) {
             if (t < t0 || t >= t1) continue;
@@ -275,46 +287,70 @@ __device__ __forceinline__ void small_gram_groups(d4 *acc, const char *tile, int
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb)
                 fr[rb] = *reinterpret_cast<const d2v *>(tile + sg_off(16 * rb + rr, 4 * t + g));
-            small_mma<NB, W, 0, NJ>(acc, fr);
+            small_mma<NB, W, J0, J1>(acc, fr);
         }
     }
 }
 
-// G item s: stage the item's columns, the MFMAs, the partials written sc1
-// (staging half the columns and computing it while the other half landed was
-// 1.3 us slower per item: one more barrier, and the item is latency-bound)
-template <typename T, bool VEC, int NB, int W>
-__device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int s, int lane, char *tile,
-                                                SmallStage<T, VEC, NB> &st) {
+// G item (chunk c, part PART): columns [KC c, KC c + KC) staged once, then
+// wave W runs part PART of its blocks b = W + 4 j (the j range cut in SPLIT
+// pieces), so the Gram's MFMAs spread over SPLIT times as many CUs while a
+// chunk's partial (one per KC columns: ~NBLK * 2 KiB written sc1, the same
+// bytes whatever KC is) is written once per KC columns; the partials written
+// sc1.  (Staging half the columns and computing it while the other half
+// landed was 1.3 us slower per item: one more barrier.)
+template <typename T, bool VEC, int NB, int W, int PART>
+__device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int c, long long *tr, int lane,
+                                                char *tile, SmallStage<T, VEC, NB> &st) {
     constexpr int NBLK = NB * (NB + 1) / 2;
     constexpr int NJ = (NBLK - W + 3) / 4;  // this wave's blocks
-    constexpr int NG = SMALL_KC / 8, H = NG / 2;
+    constexpr int J0 = PART * NJ / SMALL_SPLIT, J1 = (PART + 1) * NJ / SMALL_SPLIT;
+    constexpr int NG = SMALL_KC / 8;
     const int rr = lane & 15, g = lane >> 4;
     d4 acc[NJ > 0 ? NJ : 1];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
-    (void)H;
     st.store(tile, 0, SMALL_GR);
     __syncthreads();
-    small_gram_groups<NB, W, NJ>(acc, tile, lane, 0, NG);
+    stamp(tr, 0);
+    small_gram_groups<NB, W, J0, J1>(acc, tile, lane, 0, NG);
+    if (W == 0) {  // wave 0's MFMAs done (debug trace only)
+        if (tr && J1 > J0) asm volatile("s_nop 0" ::"v"(acc[J0][0]));
+        stamp(tr, 1);
+    }
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        double *out = a.part + ((int64_t)s * NBLK + W + 4 * j) * 256;
+    for (int j = J0; j < J1; ++j) {
+        double *out = a.part + ((int64_t)c * NBLK + W + 4 * j) * 256;
 #pragma unroll
         for (int r = 0; r < 4; ++r) st1(out + (g + 4 * r) * 16 + rr, (double)acc[j][r]);
     }
 }
 
+template <typename T, bool VEC, int NB, int W>
+__device__ __forceinline__ void small_gram_w(const SmallArgs &a, int c, int h, long long *tr,
+                                             int lane, char *tile, SmallStage<T, VEC, NB> &st) {
+    static_assert(SMALL_SPLIT == 4, "parts");
+    switch (h) {
+    case 0: small_gram_wave<T, VEC, NB, W, 0>(a, c, tr, lane, tile, st); break;
+    case 1: small_gram_wave<T, VEC, NB, W, 1>(a, c, tr, lane, tile, st); break;
+    case 2: small_gram_wave<T, VEC, NB, W, 2>(a, c, tr, lane, tile, st); break;
+    default: small_gram_wave<T, VEC, NB, W, 3>(a, c, tr, lane, tile, st); break;
+    }
+}
+
 template <typename T, bool VEC, int NB>
-__device__ __forceinline__ void small_gram(const SmallArgs &a, int s, int wave, int lane,
+__device__ __forceinline__ void small_gram(const SmallArgs &a, int it, int wave, int lane,
                                            char *tile) {
+    int c, h;
+    g_item(it, a.P, c, h);
+    long long *tr = a.trace ? a.trace + 8 * (int64_t)it : nullptr;
     SmallStage<T, VEC, NB> st;
-    st.load(a, s);
+    st.load(a, c);
     switch (wave) {
-    case 0: small_gram_wave<T, VEC, NB, 0>(a, s, lane, tile, st); break;
-    case 1: small_gram_wave<T, VEC, NB, 1>(a, s, lane, tile, st); break;
-    case 2: small_gram_wave<T, VEC, NB, 2>(a, s, lane, tile, st); break;
-    default: small_gram_wave<T, VEC, NB, 3>(a, s, lane, tile, st); break;
+    case 0: small_gram_w<T, VEC, NB, 0>(a, c, h, tr, lane, tile, st); break;
+    case 1: small_gram_w<T, VEC, NB, 1>(a, c, h, tr, lane, tile, st); break;
+    case 2: small_gram_w<T, VEC, NB, 2>(a, c, h, tr, lane, tile, st); break;
+    default: small_gram_w<T, VEC, NB, 3>(a, c, h, tr, lane, tile, st); break;
     }
 }
 
@@ -354,7 +390,7 @@ __device__ __forceinline__ void small_reduce(const SmallArgs &a, int q, int tid,
 // butterfly, the 4 waves in order -- the same sorted array and the same shape,
 // so the score is K2's bitwise (for the same U).
 __device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid, uint64_t *kbuf,
-                                             double *sbuf, int *rk, double *red) {
+                                             double *sbuf, int *rk, double *red, long long *tr) {
     const int n = a.n, lane = tid & 63, wave = tid >> 6;
     const int64_t k = n - a.f - 2 > 0 ? n - a.f - 2 : 0;
     const int e = tid & 127, h = tid >> 7;
@@ -365,6 +401,7 @@ __device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid,
         kbuf[e] = key;
     }
     __syncthreads();
+    stamp(tr, 0);
     const uint64_t key = kbuf[e];
     int cnt = 0;
 #pragma unroll
@@ -382,6 +419,7 @@ __device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid,
     __syncthreads();
     if (h == 0) sbuf[cnt + rk[e]] = dkey_inv(key);
     __syncthreads();
+    stamp(tr, 1);
     double acc = 0.0;
     if (1 + tid <= k && 1 + tid < 128) acc += sbuf[1 + tid];
 #pragma unroll
@@ -397,57 +435,65 @@ __device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid,
     }
 }
 
-// the last S item: rank, compact, margin (n <= 128, one workgroup).  Thread
-// t < n ranks row t against every key in LDS (broadcast reads); waves 0-1
-// compact the mask with ballots
-__device__ __forceinline__ void small_select(const SmallArgs &a, int wave, int lane,
-                                             uint64_t *keys, double *bnd, double *dg,
-                                             uint64_t *maskw) {
-    const int n = a.n, m = n - a.f;
-    const int tid = threadIdx.x;
+// M item c: every M item ranks the n published scores itself (n <= 128: one
+// LDS pass, no separate selection hand-off), compacts the selection with
+// ballots, and sums columns [128 c, 128 c + 128) of the m selected rows in
+// ascending order (K4's order: the same bits), every load in flight at once.
+// Item 0 also writes sel and the margin.
+template <typename T>
+__device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int wave, int lane,
+                                           uint64_t *keys, int64_t *soff, double *dg, double *bnd,
+                                           uint64_t *balw, int *rkm, char *tile, long long *tr) {
+    const int n = a.n, m = n - a.f, tid = threadIdx.x;
     double si = 0.0;
-    if (tid < n) {  // every score and diagonal in flight at once, into LDS
+    if (tid < n) {
         si = ld1(a.scores + tid);
         keys[tid] = dkey(si);
-        dg[tid] = ld1(a.diag + tid);
+    } else if (c == 0 && tid >= 128 && tid - 128 < n) {
+        dg[tid - 128] = ld1(a.diag + tid - 128);
     }
     __syncthreads();
-    bool on = false;
-    if (tid < n) {
-        const uint64_t ki = keys[tid];
-        int cnt = 0;
-        int j = 0;
-        for (; j + 8 <= n; j += 8) {
+    stamp(tr, 0);
+    // rank of row e in the (score, index) total order: threads e and 128 + e
+    // count over the two halves of the keys
+    const int e = tid & 127, h = tid >> 7;
+    int cnt = 0;
+    uint64_t ki = 0;
+    if (e < n) {
+        ki = keys[e];
+        const int j1 = n < 64 * h + 64 ? n : 64 * h + 64;
+        int j = 64 * h;
+        for (; j + 8 <= j1; j += 8) {
             uint64_t o[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) o[u] = keys[j + u];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) cnt += (o[u] < ki) || (o[u] == ki && j + u < tid);
+            for (int u = 0; u < 8; ++u) cnt += (o[u] < ki) || (o[u] == ki && j + u < e);
         }
-        for (; j < n; ++j) {
+        for (; j < j1; ++j) {
             const uint64_t o = keys[j];
-            cnt += (o < ki) || (o == ki && j < tid);
+            cnt += (o < ki) || (o == ki && j < e);
         }
+    }
+    if (h == 1 && e < n) rkm[e] = cnt;
+    __syncthreads();
+    bool on = false;
+    if (h == 0 && e < n) {
+        cnt += rkm[e];
         on = cnt < m;
-        if (cnt == m - 1) bnd[0] = si;
-        if (cnt == m) bnd[1] = si;
+        if (c == 0 && cnt == m - 1) bnd[0] = si;
+        if (c == 0 && cnt == m) bnd[1] = si;
     }
-    if (tid < 3) maskw[tid] = 0;
-    __syncthreads();
-    if (on) atomicOr(reinterpret_cast<unsigned long long *>(&maskw[tid / 63]), 1ull << (tid % 63));
-    __syncthreads();
     // compaction: rows 0..63 in wave 0, 64..127 in wave 1
-    __shared__ int wcount;
-    if (wave < 2) {
-        const uint64_t bal = __ballot(on);
-        if (wave == 0 && lane == 0) wcount = __popcll(bal);
-        __syncthreads();
-        const int pos = (wave ? wcount : 0) + __popcll(bal & ((1ull << lane) - 1));
-        if (on) st1(a.sel + pos, (int64_t)tid);
-    } else {
-        __syncthreads();
+    const uint64_t bal = __ballot(on);
+    if (wave < 2 && lane == 0) balw[wave] = bal;
+    __syncthreads();
+    if (on) {
+        const int pos = (wave ? __popcll(balw[0]) : 0) + __popcll(bal & ((1ull << lane) - 1));
+        soff[pos] = (int64_t)tid * a.ld;
+        if (c == 0 && a.sel) a.sel[pos] = (int64_t)tid;
     }
-    if (wave == 0) {
+    if (c == 0 && wave == 3) {
         double M = 0.0;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -464,66 +510,58 @@ __device__ __forceinline__ void small_select(const SmallArgs &a, int wave, int l
             write_margin(a.margin, bnd[0], bnd[1], M, (double)a.d, k, 0x1p-53);
         }
     }
-}
-
-// M item c: mean of columns [256 c, 256 c + 256): each thread one column, the
-// m selected rows in ascending order (K4's order: the same bits)
-template <typename T>
-__device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int tid, int64_t *soff,
-                                           const uint64_t *maskw) {
-    const int m = a.n - a.f;
-    if (__popcll(maskw[0]) + __popcll(maskw[1]) + __popcll(maskw[2]) != m) {
-        // never index X with a damaged mask: report (BK_EHIP) and skip
-        if (tid == 0)
-            __hip_atomic_fetch_or(cline(a.ctr, C_ERR), 2u, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    if (tid < a.n) {  // ascending selected rows from the mask the flag carried
-        const int w = tid / 63, b = tid % 63;
-        if ((maskw[w] >> b) & 1) {
-            int pos = __popcll(maskw[w] & ((1ull << b) - 1));
-            for (int u = 0; u < w; ++u) pos += __popcll(maskw[u]);
-            soff[pos] = (int64_t)tid * a.ld;
-        }
+    __syncthreads();
+    stamp(tr, 1);
+    if (!a.mean) return;
+    // the selected rows' offsets in registers (lane u: selected row u, or
+    // 64 + u in waves 2-3; lanes past m repeat row m - 1, so every load is
+    // valid), read with v_readlane per load instead of a broadcast LDS read +
+    // wait per load.  v_readlane ignores EXEC, so no lane may skip the offset
+    // loads: every lane runs the loads (columns past d clamped to the last one)
+    // and only the store is conditional.  mm (= m) is re-derived from LDS so
+    // the per-row tests stay inside the item (hoisted out of the item loop,
+    // 64 loop-invariant masks were spilled and cost ~4 us per item).
+    // Waves 0-1 load rows 0..63 of the item's 128 columns, waves 2-3 rows
+    // 64..m-1 at the same time into LDS (the G tile: (m - 64) KiB <= 8 NB KiB);
+    // waves 0-1 then add them in order: K4's ascending sum, bit for bit
+    const int mm = __popcll(balw[0]) + __popcll(balw[1]);
+    const int cl = e;  // (e = tid & 127, h = tid >> 7 as in the rank)
+    const int64_t col = (int64_t)c * 128 + cl;
+    const T *X = (const T *)a.X + (col < a.d ? col : a.d - 1);
+    double *spill = reinterpret_cast<double *>(tile);  // [row - 64][128]
+    const int64_t o = soff[64 * h + lane < mm ? 64 * h + lane : mm - 1];
+    double acc = 0.0;
+    if (h == 0) {
+        double v[64];
+#pragma unroll
+        for (int u = 0; u < 64; ++u) v[u] = (double)X[__builtin_amdgcn_readlane((long long)o, u)];
+#pragma unroll
+        for (int u = 0; u < 64; ++u) acc = u < mm ? acc + v[u] : acc;
+    } else if (mm > 64) {
+        double v[64];
+#pragma unroll
+        for (int u = 0; u < 64; ++u) v[u] = (double)X[__builtin_amdgcn_readlane((long long)o, u)];
+#pragma unroll
+        for (int u = 0; u < 64; ++u)
+            if (64 + u < mm) spill[u * 128 + cl] = v[u];
     }
     __syncthreads();
-    const int64_t col = (int64_t)c * 256 + tid;
-    if (col < a.d) {
-        const T *X = (const T *)a.X;
-        double acc = 0.0;
-        int r = 0;
-        for (; r + 64 <= m; r += 64) {  // 64 loads in flight per thread
-            double v[64];
-#pragma unroll
-            for (int u = 0; u < 64; ++u) v[u] = (double)X[soff[r + u] + col];
-#pragma unroll
-            for (int u = 0; u < 64; ++u) acc += v[u];
-        }
-        if (r < m) {  // the rest, also in flight together
-            double v[64];
-#pragma unroll
-            for (int u = 0; u < 64; ++u) v[u] = r + u < m ? (double)X[soff[r + u] + col] : 0.0;
-#pragma unroll
-            for (int u = 0; u < 64; ++u)
-                if (r + u < m) acc += v[u];
-            r = m;
-        }
-        for (; r < m; ++r) acc += (double)X[soff[r] + col];
-        a.mean[col] = acc / (double)m;
+    if (h == 0) {
+        for (int u = 64; u < mm; ++u) acc += spill[(u - 64) * 128 + cl];
+        if (col < a.d) a.mean[col] = acc / (double)m;
     }
 }
 
 template <typename T>
 __device__ __forceinline__ void small_prefetch(const SmallArgs &a, int c, int tid) {
-    const int64_t col = (int64_t)c * 256 + tid;
-    if (col >= a.d) return;
+    const int64_t col = (int64_t)c * 128 + (tid & 127);
+    if (!a.mean || col >= a.d) return;
     const T *X = (const T *)a.X;
     T acc = 0;
-    for (int r = 0; r < a.n; r += 16) {
+    for (int r = tid >> 7; r < a.n; r += 32) {
         T v[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = r + u < a.n ? X[(int64_t)(r + u) * a.ld + col] : (T)0;
+        for (int u = 0; u < 16; ++u) v[u] = r + 2 * u < a.n ? X[(int64_t)(r + 2 * u) * a.ld + col] : (T)0;
 #pragma unroll
         for (int u = 0; u < 16; ++u) acc += v[u];
     }
@@ -542,68 +580,74 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     __shared__ double bnd[2];
     __shared__ double dgl[128];
     __shared__ int64_t soff[128];
-    __shared__ uint64_t maskw[3];
+    __shared__ uint64_t balw[2];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int total = a.P + a.Q + a.n + a.C;
+    const int NGI = SMALL_SPLIT * a.P;  // G items: SPLIT per chunk
+    const int total = NGI + a.Q + a.n + a.C;
     unsigned *ctr = a.ctr;
-    for (;;) {
-        if (tid == 0)
-            s_item = (int)__hip_atomic_fetch_add(cline(ctr, C_HEAD), 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
+    // the first S0 items (G items) go to workgroups by blockIdx, the rest in
+    // queue order (one returning atomic each): 256 dequeues on one counter
+    // take ~3 us, which delayed the last G item's start by that much
+    const int S0 = NGI < (int)gridDim.x ? NGI : (int)gridDim.x;
+    bool last_out = false;
+    for (bool first = true;; first = false) {
+        if (first && (int)blockIdx.x < S0) {
+            if (tid == 0) s_item = (int)blockIdx.x;
+        } else if (tid == 0) {
+            s_item = S0 + (int)__hip_atomic_fetch_add(cline(ctr, C_HEAD), 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+        }
         __syncthreads();
         const int it = s_item;
         __syncthreads();
-        if (it >= total) break;
+        if (it >= total) {
+            // every workgroup ends on exactly one failed dequeue; the last of
+            // them (its add returned total - S0 + grid - 1) is the last one out
+            last_out = it == total + (int)gridDim.x - 1;
+            break;
+        }
         long long t0 = 0, m0 = 0;
         if (a.trace && tid == 0) {
             t0 = (long long)__builtin_amdgcn_s_memrealtime();
             m0 = (long long)__builtin_amdgcn_s_memtime();
         }
-        if (it < a.P) {
+        if (it < NGI) {
             small_gram<T, VEC, NB>(a, it, wave, lane, tile);
-            if (wg_arrive(ctr, C_G, (unsigned)a.P, &s_old)) wg_raise(ctr, F_G);
-        } else if (it < a.P + a.Q) {
+            if (wg_arrive(ctr, C_G, G_GRP, it, NGI, &s_old)) wg_raise(ctr, F_G);
+        } else if (it < NGI + a.Q) {
             wg_wait_flag(ctr, F_G);
-            if (a.trace && tid == 0) a.trace[6 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-            small_reduce(a, it - a.P, tid, NB, red);
-            if (wg_arrive(ctr, C_R, (unsigned)a.Q, &s_old)) wg_raise(ctr, F_R);
-        } else if (it < a.P + a.Q + a.n) {
+            if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+            small_reduce(a, it - NGI, tid, NB, red);
+            if (wg_arrive(ctr, C_R, R_GRP, it - NGI, a.Q, &s_old)) wg_raise(ctr, F_R);
+        } else if (it < NGI + a.Q + a.n) {
             wg_wait_flag(ctr, F_R);
-            if (a.trace && tid == 0) a.trace[6 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-            small_scores(a, it - a.P - a.Q, tid, kbuf, sbuf, rk, &red[0][0]);
-            if (wg_arrive(ctr, C_S, (unsigned)a.n, &s_old)) {
-                // the last S item: every score and diagonal is published;
-                // small_select reads them sc1
-                small_select(a, wave, lane, kbuf, bnd, dgl, maskw);
-                uint64_t w3[3] = {maskw[0], maskw[1], maskw[2]};
-                sel_raise(ctr, w3);
-            }
+            if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+            small_scores(a, it - NGI - a.Q, tid, kbuf, sbuf, rk, &red[0][0],
+                         a.trace ? a.trace + 8 * it : nullptr);
+            if (wg_arrive(ctr, C_S, S_GRP, it - NGI - a.Q, a.n, &s_old)) wg_raise(ctr, F_S);
         } else {
-            // while the selection is computed: pull this item's columns of
+            // while the scores are computed: pull this item's columns of
             // every row toward this XCD's L2, so the mean's loads hit it
-            small_prefetch<T>(a, it - a.P - a.Q - a.n, tid);
-            sel_wait(ctr, maskw);
-            if (a.trace && tid == 0) a.trace[6 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-            small_mean<T>(a, it - a.P - a.Q - a.n, tid, soff, maskw);
+            small_prefetch<T>(a, it - NGI - a.Q - a.n, tid);
+            wg_wait_flag(ctr, F_S);
+            if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
+            small_mean<T>(a, it - NGI - a.Q - a.n, wave, lane, kbuf, soff, dgl, bnd, balw, rk, tile,
+                          a.trace ? a.trace + 8 * it : nullptr);
         }
         if (a.trace && tid == 0) {
             unsigned hw;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            a.trace[6 * it] = t0;
-            a.trace[6 * it + 2] = (long long)__builtin_amdgcn_s_memrealtime();
-            a.trace[6 * it + 3] = (long long)hw | ((long long)blockIdx.x << 32);
-            a.trace[6 * it + 4] = m0;
-            a.trace[6 * it + 5] = (long long)__builtin_amdgcn_s_memtime();
+            a.trace[8 * it] = t0;
+            a.trace[8 * it + 2] = (long long)__builtin_amdgcn_s_memrealtime();
+            a.trace[8 * it + 3] = (long long)hw | ((long long)blockIdx.x << 32);
+            a.trace[8 * it + 4] = m0;
+            a.trace[8 * it + 5] = (long long)__builtin_amdgcn_s_memtime();
         }
     }
     // the last workgroup out resets the queue for the next launch (stream
     // order: the next launch starts after this one has completed) -- every
-    // word of every line: the F_SEL lines carry the mask in words 0..5
-    if (tid == 0)
-        s_old = __hip_atomic_fetch_add(cline(ctr, C_EXIT), 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (s_old == gridDim.x - 1) {
+    // word of every line
+    if (last_out) {
         if (tid == 0 && ctr_load(cline(ctr, C_ERR))) {  // a wait gave up: outputs invalid
             a.margin[0] = __builtin_nan("");
             a.margin[2] = 2.0;  // read_margin reports BK_EHIP
@@ -636,9 +680,10 @@ SmallPlan small_plan(int n, int64_t d, int num_cu) {
     const int64_t kc = SMALL_KC;
     p.kc = (int)kc;
     p.P = (int)((d + kc - 1) / kc);
+    p.ng = SMALL_SPLIT * p.P;
     p.Q = 4 * p.nblk;
     p.nS = n;  // one S item per row
-    p.C = (int)((d + 255) / 256);
+    p.C = (int)((d + 127) / 128);
     return p;
 }
 
@@ -657,7 +702,7 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     a.P = p.P;
     a.Q = p.Q;
     a.nS = p.nS;
-    a.C = mean ? p.C : 0;
+    a.C = mean ? p.C : 1;  // item 0 writes sel and the margin even without a mean
     a.nblk = p.nblk;
     a.T = (n + 63) / 64;
     a.part = part;
@@ -668,7 +713,7 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     a.margin = margin;
     a.sel = sel;
     a.ctr = ctr;
-    const int total = a.P + a.Q + a.n + a.C;
+    const int total = SMALL_SPLIT * a.P + a.Q + a.n + a.C;
     const int grid = total < num_cu ? total : num_cu;
     const bool vec = (ld % 2) == 0 && ((uintptr_t)X % (dtype == 0 ? 16 : 8)) == 0;
     if (dtype == 0 && vec)

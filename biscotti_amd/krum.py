@@ -322,6 +322,10 @@ class Engine:
             mask |= 1 << _lib.K[k]
         check(lib().bk_timing_select(self._ctx, mask))
 
+    def timing_stride(self, every):
+        """Record a timed kernel's events on every `every`-th launch (bk_timing_stride)."""
+        check(lib().bk_timing_stride(self._ctx, int(every)))
+
     def timing_read(self):
         out = {}
         for i, name in enumerate(_lib.KERNELS):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 7
+#define BK_ABI_VERSION 8
 
 typedef struct bk_ctx bk_ctx;
 
@@ -328,6 +328,12 @@ int bk_timing_enable(bk_ctx *ctx, int on);   /* all kernels; clears accumulated 
  * adds two event records to the stream.  Clears accumulated timings. */
 int bk_timing_select(bk_ctx *ctx, uint32_t kernel_mask);
 int bk_timing_read(bk_ctx *ctx, int kernel_id, double *total_ms, int64_t *count);
+/* Record the events of a timed kernel on every `every`-th launch only (1, the
+ * default: every launch).  Two event records cost a few us of stream time, as
+ * much as config B's whole one-launch step: sampling keeps the timed region's
+ * step time honest while the kernel is still timed live.  Clears accumulated
+ * timings. */
+int bk_timing_stride(bk_ctx *ctx, int every);
 const char *bk_kernel_name(int kernel_id);
 /* The K1 plan for an aligned fp64 shape: S = workgroup groups (row-block
  * sets, bk_plan.hip), kc = columns per k-block, ntile = 64x64 upper sub-tiles,

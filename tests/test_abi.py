@@ -41,7 +41,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_names():
     L = _lib.lib()
-    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 7
+    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 8
     assert L.bk_kernel_name(0) == b"k_gram"
     assert L.bk_kernel_name(99) == b"?"
     assert len(_lib.KERNELS) == 16
@@ -125,6 +125,7 @@ def test_null_and_bad_arguments_do_not_crash():
     assert L.bk_comm_size(None, None, None) == _lib.BK_EINVAL
     assert L.bk_comm_stats(None, None, None) == _lib.BK_EINVAL
     assert L.bk_set_small_path(None, 1) == _lib.BK_EINVAL
+    assert L.bk_timing_stride(None, 2) == _lib.BK_EINVAL
     assert L.bk_multikrum_sharded_device(None, None, 0, 10, 0, 0, 2, None, None,
                                          None) == _lib.BK_EINVAL
 

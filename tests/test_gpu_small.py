@@ -134,3 +134,22 @@ def test_small_optional_outputs(engine, oracle):
     assert np.array_equal(s1, full[0])
     s2, _, m2 = _run(engine, X, 30, scores=False)
     assert np.array_equal(m2.view(np.uint8), full[2].view(np.uint8))
+
+
+def test_timing_stride_samples_launches(engine, oracle):
+    """bk_timing_stride: the bench's timed region events every 10th k_small."""
+    n, d, f = 40, 300, 10
+    X = oracle.synth(n, d, 11, 8)
+    Xd = torch.from_numpy(X).cuda()
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    try:
+        engine.timing_select(["k_small"])
+        engine.timing_stride(4)
+        for _ in range(9):
+            engine.multikrum_device_ptr(Xd.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr())
+        engine.synchronize()
+        t = engine.timing_read()
+        assert t["k_small"]["count"] == 3  # launches 0, 4, 8
+    finally:
+        engine.timing_stride(1)
+        engine.timing_select([])

@@ -30,9 +30,9 @@ raw = np.fromfile(sys.argv[1], dtype=np.int64)
 pos, calls = 0, []
 while pos < len(raw):
     items, P, Q, nS, C = raw[pos:pos + 5]
-    tr = raw[pos + 5:pos + 5 + 6 * items].reshape(items, 6)
+    tr = raw[pos + 5:pos + 5 + 8 * items].reshape(items, 8)
     calls.append((P, Q, nS, C, tr))
-    pos += 5 + 6 * items
+    pos += 5 + 8 * items
 P, Q, nS, C, tr = calls[-1]
 t0 = tr[:, 0][tr[:, 0] > 0].min()
 us = lambda x: (x - t0) / 100.0  # s_memrealtime: 100 MHz
@@ -45,6 +45,11 @@ for name, a, b in kinds:
     work = en - np.where(seg[:, 1] > 0, wt, st)
     print("%s items %3d: start %6.2f..%6.2f  waited-until %6.2f..%6.2f  end %6.2f..%6.2f  work med %.2f max %.2f us"
           % (name, b - a, st.min(), st.max(), (wt.min() if name != "G" else 0), (wt.max() if name != "G" else 0), en.min(), en.max(), np.median(work), work.max()))
+    if (seg[:, 6] > 0).all() and (seg[:, 7] > 0).all():
+        s0, s1 = us(seg[:, 6]), us(seg[:, 7])
+        b0 = np.where(seg[:, 1] > 0, wt, st)
+        print("    in-item stages (median us): to stamp 0 %.2f, stamp 0->1 %.2f, stamp 1->end %.2f"
+              % (np.median(s0 - b0), np.median(s1 - s0), np.median(en - s1)))
 clk = (tr[:, 5] - tr[:, 4]) / np.maximum(1, tr[:, 2] - tr[:, 0]) * 100 / 1000.0
 print("shader clock (GHz) over items: median %.2f min %.2f" % (np.median(clk[clk > 0]), clk[clk > 0].min()))
 print("calls traced: %d; last call span %.2f us" % (len(calls), us(tr[:, 2]).max()))
