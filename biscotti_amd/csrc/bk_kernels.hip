@@ -1254,15 +1254,18 @@ __device__ __forceinline__ void k2_sort16(K (&v)[16], K *lds, int N, int tid) {
 }
 
 // v1's summation shape over the sorted keys (virtual thread t' = tid + NT h)
+// ranks >= nfin hold NaN (v1's keys sort NaN after +inf; v2/v3 sort the NaN
+// distances as +inf and put the NaN back here, at the same ranks)
 template <typename K, int NT, int NT_SUM, bool PAD = false>
-__device__ __forceinline__ double k2_sum(const K *keys_lds, int64_t k, int tid, double *red) {
+__device__ __forceinline__ double k2_sum(const K *keys_lds, int64_t k, int tid, double *red,
+                                         int64_t nfin = INT64_MAX) {
     constexpr int H = NT_SUM / NT;
     const int lane = tid & 63;
 #pragma unroll
     for (int h = 0; h < H; ++h) {
         double acc = 0.0;
         for (int64_t r = 1 + tid + NT * h; r <= k; r += NT_SUM)
-            acc += K2Ord<K>::val(keys_lds[PAD ? k2_pad((int)r) : r]);
+            acc += r < nfin ? K2Ord<K>::val(keys_lds[PAD ? k2_pad((int)r) : r]) : __builtin_nan("");
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if (lane == 0) red[(tid >> 6) + (NT / 64) * h] = acc;
@@ -1303,10 +1306,18 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
     const double di = TR ? dg_in[i] : u_at(U, T_, i, i);
     if (tid == 0) diag[i] = di;
     // distances, element e = tid + NT q (consecutive lanes, consecutive
-    // columns: coalesced row reads), through LDS into the blocked layout
+    // columns: coalesced row reads), through LDS into the blocked layout.  A
+    // NaN distance sorts as +inf and is counted: v1's order puts the row's
+    // NaNs right after every +inf and before the padding, i.e. at ranks
+    // n - nan .. n - 1, and k2_sum adds NaN there -- the same scores, bitwise,
+    // without a second (u64-key) sort in the kernel (its registers held K2 at
+    // 3 waves per SIMD)
     constexpr bool V3 = KPT == 16;  // the register-local sort (k2_sort16)
+    __shared__ int s_nan;
+    if (tid == 0) s_nan = 0;
+    __syncthreads();
     double *kd = reinterpret_cast<double *>(keys);
-    bool nan = false;
+    int nanc = 0;
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
         const int e = tid + NT * q;
@@ -1318,7 +1329,10 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
             const double g2 = 2.0 * k2_g<TR>(U, Ut, T_, i, e);
             x = t - g2;
             x = x == 0.0 ? 0.0 : x;  // -0 == +0 (v1's dkey)
-            nan |= x != x;
+            if (x != x) {
+                ++nanc;
+                x = __builtin_inf();
+            }
         }
         kd[V3 ? k2_pad(e) : e] = x;
     }
@@ -1326,6 +1340,7 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
         if (kd[tid] == 1.2345) scores[i] = kd[tid];  // keep the loads
         return;
     }
+    if (nanc) atomicAdd(&s_nan, nanc);
     __syncthreads();
     double dv[KPT];
     if constexpr (V3) {
@@ -1334,27 +1349,15 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
 #pragma unroll
         for (int q = 0; q < KPT; ++q) dv[q] = kd[tid * KPT + q];
     }
+    const int64_t nfin = n - s_nan;
+    __syncthreads();  // kd[] reads before the sort's writes
     double sum;
-    if (!__syncthreads_or(nan)) {  // (the barrier also orders kd[] reads before the sort's writes)
-        if constexpr (V3) {
-            k2_sort16<double>(dv, kd, N, tid);
-            sum = k2_sum<double, NT, NT_SUM, true>(kd, k, tid, red);
-        } else {
-            k2_sort<double, NT, KPT>(dv, kd, N, tid);
-            sum = k2_sum<double, NT, NT_SUM>(kd, k, tid, red);
-        }
-    } else {  // a NaN in the row: v1's order-preserving keys, NaN last
-        uint64_t v[KPT];
-#pragma unroll
-        for (int q = 0; q < KPT; ++q)
-            v[q] = tid * KPT + q < n ? dkey(dv[q]) : ~0ULL;
-        if constexpr (V3) {
-            k2_sort16<uint64_t>(v, keys, N, tid);
-            sum = k2_sum<uint64_t, NT, NT_SUM, true>(keys, k, tid, red);
-        } else {
-            k2_sort<uint64_t, NT, KPT>(v, keys, N, tid);
-            sum = k2_sum<uint64_t, NT, NT_SUM>(keys, k, tid, red);
-        }
+    if constexpr (V3) {
+        k2_sort16<double>(dv, kd, N, tid);
+        sum = k2_sum<double, NT, NT_SUM, true>(kd, k, tid, red, nfin);
+    } else {
+        k2_sort<double, NT, KPT>(dv, kd, N, tid);
+        sum = k2_sum<double, NT, NT_SUM>(kd, k, tid, red, nfin);
     }
     if (tid == 0) scores[i] = (k > 0) ? sum : 0.0;
 }

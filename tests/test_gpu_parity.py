@@ -309,15 +309,20 @@ def test_exact_ties_bitwise(engine, oracle, n):
         assert np.array_equal(sc, osc), (n, f)
 
 
-def test_nan_and_inf_rows(engine, oracle):
+@pytest.mark.parametrize("n", [200, 2100, 4500])
+def test_nan_and_inf_rows(engine, oracle, n):
     """NaN / Inf rows: NaN-aware score agreement with the oracle and the same
-    selection (NaN sorts last, as in numpy)."""
+    selection (NaN sorts last, as in numpy).  n = 200 runs K2's lane-exchange
+    sort, 2100 and 4500 the register-local one on transposed rows (16 keys
+    per thread, 4096 / 8192 keys), where NaN distances sort as +inf and are
+    put back at ranks n - #NaN .. n - 1."""
     rng = np.random.default_rng(5)
-    X = rng.standard_normal((200, 64))
+    X = rng.standard_normal((n, 64))
     X[7] = np.nan
     X[50, 3] = np.inf
     X[120] = -np.inf
-    for f in (20, 60, 150):
+    X[n - 3, 10] = np.nan
+    for f in (n // 10, 3 * n // 10, 3 * n // 4):
         sel, sc, _ = engine.multikrum(X, f)
         osel, osc, _ = oracle.krum(X, f)
         assert np.array_equal(sel, osel)

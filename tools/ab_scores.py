@@ -21,6 +21,8 @@ def load(path):
             fn.restype, fn.argtypes = res, args
     ctx = ctypes.c_void_p()
     assert lib.bk_create(ctypes.byref(ctx), 0) == 0
+    if hasattr(lib, "bk_set_small_path"):  # K2 is the subject: n <= 128 through the chain too
+        assert lib.bk_set_small_path(ctx, 0) == 0
     return lib, ctx
 
 
