@@ -39,24 +39,42 @@ def pass_durations(d):
     return out
 
 
-def load_pmc(d):
+def load_pmc(d, only=None):
     """Per kernel: mean of every counter over its dispatches, plus the physical
     shader clock per dispatch, GRBM_GUI_ACTIVE / 8 XCDs / that dispatch's own
-    duration in the same pass (MI355X_MICROARCH.md, DVFS give-back)."""
+    duration in the same pass (MI355X_MICROARCH.md, DVFS give-back).
+    only(kernel, duration_ms, longest_ms_of_kernel_in_pass) -> keep the dispatch?"""
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     clocks = collections.defaultdict(list)
+    durs = collections.defaultdict(list)
     for sub in sorted(os.listdir(d)):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not sub.startswith("pmc") or not os.path.exists(p):
             continue
         dur = pass_durations(os.path.join(d, sub))
-        for r in csv.DictReader(open(p)):
-            k = short(r["Kernel_Name"])
-            agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        rows = list(csv.DictReader(open(p)))
+        longest = collections.defaultdict(float)
+        for r in rows:
             t = dur.get(r.get("Dispatch_Id"))
+            if t:
+                k = short(r["Kernel_Name"])
+                longest[k] = max(longest[k], t)
+        seen = set()
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            t = dur.get(r.get("Dispatch_Id"))
+            if only is not None and not only(k, t or 0.0, longest[k]):
+                continue
+            agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if t and (sub, r.get("Dispatch_Id")) not in seen:
+                seen.add((sub, r.get("Dispatch_Id")))
+                durs[k].append(t)
             if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and t:
                 clocks[k].append(float(r["Counter_Value"]) / 8.0 / (t * 1e-3) / 1e9)
     res = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
+    for k, v in durs.items():
+        res[k]["_dispatch_ms_mean"] = sum(v) / len(v)
+        res[k]["_dispatches"] = len(v)
     for k, v in clocks.items():
         v = sorted(v)
         res[k]["_clock_ghz_median"] = v[len(v) // 2]
@@ -103,10 +121,37 @@ def main():
             k, c["FETCH_SIZE"], rd, c.get("WRITE_SIZE", 0.0), rd + wr, hr, mb, clk))
     lines += ["", "FETCH_SIZE doubled (x2) for wide 16-B/lane reads per MI355X_MICROARCH.md §HBM;",
               "WRITE_SIZE as reported.  MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)."]
+    # K1 of the workload only: its dispatches within 2x of the longest k_gram
+    # dispatch of each pass (bench.py also runs config B's chain, 500 launches
+    # of ~20 us on the same grid, which an all-dispatch mean would average in)
+    big = load_pmc(prof, only=lambda k, t, tmax: not k.startswith("k_gram") or t >= 0.5 * tmax)
+    k1p = next((k for k in big if k.startswith("k_gram") and "FETCH_SIZE" in big[k]), None)
+    if k1p:
+        c = big[k1p]
+        gui = c.get("GRBM_GUI_ACTIVE", 0.0)
+        sc = gui / 8.0 * 1024 if gui else 0
+        rd = c["FETCH_SIZE"] * 1024.0 * 2.0
+        wr = c.get("WRITE_SIZE", 0.0) * 1024.0
+        hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
+        pmc_k1 = dict(fetch_kib=c["FETCH_SIZE"], read_bytes_corrected=rd, write_bytes=wr,
+                      hbm_bytes_per_launch=rd + wr,
+                      tcc_hit_pct=100.0 * hit / (hit + miss) if hit + miss else float("nan"),
+                      mfma_busy_pct=100.0 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / sc if sc else float("nan"),
+                      clock_ghz=c.get("_clock_ghz_median", float("nan")), fetch_correction=2.0,
+                      pmc_dispatch_ms_mean=c.get("_dispatch_ms_mean"),
+                      pmc_dispatches=c.get("_dispatches"))
+        lines += ["", "K1 of the workload only (%s dispatches >= half the longest of their pass; %d over the PMC passes, "
+                  "mean %.3f ms): HBM bytes/launch %.4g (read %.4g corrected, write %.4g), TCC hit %.1f%%, "
+                  "MFMA busy %.1f%%, clock %.2f GHz" % (k1p, pmc_k1["pmc_dispatches"],
+                                                      pmc_k1["pmc_dispatch_ms_mean"], rd + wr, rd, wr,
+                                                      pmc_k1["tcc_hit_pct"], pmc_k1["mfma_busy_pct"],
+                                                      pmc_k1["clock_ghz"])]
     k1 = next((k for k in res if k.startswith("k_gram")), None)
     out_json = {"workload": workload, "source": prof, "kernels": res}
     if k1:
-        out_json["k_gram"] = res[k1]
+        out_json["k_gram"] = dict(res[k1])
+        if k1p:
+            out_json["k_gram"].update(pmc_k1)
         tr = os.path.join(prof, "trace", "run_kernel_trace.csv")
         if len(sys.argv) > 5 and os.path.exists(tr):
             w, st = int(sys.argv[4]), int(sys.argv[5])
@@ -116,6 +161,7 @@ def main():
             if win:
                 res[k1]["dispatch_ms"] = durs
                 res[k1]["timed_window_avg_ms"] = sum(win) / len(win)
+                out_json["k_gram"]["timed_window_avg_ms"] = sum(win) / len(win)
                 lines += ["", "%s per dispatch (ms): %s" % (k1, " ".join("%.3f" % x for x in durs)),
                           "timed window (dispatches %d..%d, = bench.py's timed steps): avg %.3f ms"
                           % (w + 1, w + st, sum(win) / len(win))]
@@ -124,14 +170,14 @@ def main():
     sha = hashlib.sha256(open(os.path.join(repo, "biscotti_amd", "libbk.so"), "rb").read()).hexdigest()[:16]
     out_json["libbk_sha16"] = sha
     json.dump(out_json, open(out + ".json", "w"), indent=1)
-    if k1 and "hbm_bytes_per_launch" in res[k1]:
+    if k1 and "hbm_bytes_per_launch" in out_json["k_gram"]:
         # the file bench.py reads its roofline "traffic" from (only while the
         # library hash matches: bench.py checks libbk_sha16)
         pj = os.path.join(repo, "profiles", "pmc_%s.json" % workload)
         json.dump({"workload": workload, "source": "%s.json (tools/profile.sh %s)"
                    % (os.path.relpath(out, repo), os.path.basename(prof)),
                    "libbk_sha16": sha,
-                   "k_gram": {k: v for k, v in res[k1].items() if k != "dispatch_ms"}},
+                   "k_gram": {k: v for k, v in out_json["k_gram"].items() if k != "dispatch_ms"}},
                   open(pj, "w"), indent=1)
     open(out + ".md", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
