@@ -454,7 +454,9 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
         CHK(ensure(c->small_ctr, SMALL_CTR_WORDS * sizeof(unsigned)));
         HIPCHK(hipMemsetAsync(c->small_ctr.p, 0, SMALL_CTR_WORDS * sizeof(unsigned), c->stream));
     }
-    CHK(ensure(c->small_part, (size_t)sp.P * sp.nblk * 256 * sizeof(double)));
+    // per chunk: the full-square partial Gram (16 nb16)^2 + its diagonal (bk_small.hip)
+    const size_t np16 = (size_t)16 * sp.nb16;
+    CHK(ensure(c->small_part, (size_t)sp.P * (np16 * np16 + np16) * sizeof(double)));
     CHK(ensure(c->U, (size_t)bk_upper_elems(n) * sizeof(double)));
     CHK(ensure(c->diag, (size_t)n * sizeof(double)));
     CHK(ensure(c->margin, 8 * sizeof(double)));
@@ -465,10 +467,12 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
     }
     long long *trace = nullptr;
     const int items = sp.ng + sp.Q + sp.nS + (d_mean ? sp.C : 1);
+    const int grid = items < c->num_cu ? items : c->num_cu;  // = launch_small's grid
+    const size_t twords = (size_t)items * 8 + (size_t)grid * 2;  // + per workgroup {entry, exit}
     const char *tfile = getenv("BK_SMALL_TRACE");  // debug: per-item timeline
     if (tfile) {
-        CHK(ensure(c->trace, (size_t)items * 8 * sizeof(long long)));
-        HIPCHK(hipMemsetAsync(c->trace.p, 0, (size_t)items * 8 * sizeof(long long), c->stream));
+        CHK(ensure(c->trace, twords * sizeof(long long)));
+        HIPCHK(hipMemsetAsync(c->trace.p, 0, twords * sizeof(long long), c->stream));
         trace = (long long *)c->trace.p;
     }
     CHK(timed(c, BK_K_SMALL, [&] {
@@ -479,13 +483,14 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
     }));
     c->margin_valid = 1;
     if (tfile) {
-        std::vector<long long> h((size_t)items * 8 + 5);
+        std::vector<long long> h(twords + 6);
         h[0] = items;
         h[1] = sp.ng;  // G items
         h[2] = sp.Q;
         h[3] = sp.nS;
         h[4] = d_mean ? sp.C : 1;
-        HIPCHK(hipMemcpyAsync(h.data() + 5, trace, (size_t)items * 8 * sizeof(long long),
+        h[5] = grid;
+        HIPCHK(hipMemcpyAsync(h.data() + 6, trace, twords * sizeof(long long),
                               hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (FILE *fp = fopen(tfile, "ab")) {

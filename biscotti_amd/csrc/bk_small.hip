@@ -11,13 +11,16 @@
 //   G items  (4 per 128    split-K Gram partial of 128 columns: a quarter of
 //             columns)     the upper 16x16 blocks of the (n <= 128) Gram
 //                          each, fp64 MFMA
-//   R items  (4 per block) fixed-order sum of the P partials -> packed upper U
-//   S items  (one per row) distances, sort by counting, sum of ranks 1..k in
-//                          K2's exact shape
-//   M items  (128 columns) rank the n scores (each item itself: no serial
-//                          selection step), compact the selection, mean of
-//                          the selected rows ascending (K4's order); item 0
-//                          writes sel and the margin
+//   S items  (one per row) the row's Gram entries and the diagonal summed
+//                          over the P partials in a fixed order (no separate
+//                          reduce phase), distances, sort by counting, sum of
+//                          ranks 1..k in K2's exact shape
+//   M items  (64 columns)  stage the item's columns of every row in LDS while
+//                          the scores are computed; then rank the n scores
+//                          (each item itself: no serial selection step),
+//                          compact the selection, mean of the selected rows
+//                          ascending from LDS (K4's order); item 0 writes sel
+//                          and the margin
 //
 // The first G items go to workgroups 0.. by blockIdx, the rest are dequeued
 // in order.  An item only waits (a relaxed sc1 poll of a counter) for items
@@ -43,11 +46,12 @@
 namespace bk {
 
 // queue words, each on a 128-B line of its own: the item head, the top
-// arrival counters of the G, R and S phases, a spare line, the error word;
-// then the "phase done" flags F_G, F_R, F_S, each replicated once per XCD (a
-// waiting workgroup polls its own XCD's copy: 1/8 of the pollers on any
-// line); then the arrival counters of groups of 32 items (G_GRP: up to 1024 G
-// items, R_GRP: 144 R items, S_GRP: 128 S items).  Same-address atomics
+// arrival counters of the G and S phases (C_R, F_R, R_GRP: the lines of the
+// former reduce phase, unused since S items sum the partials themselves), a
+// spare line, the error word; then the "phase done" flags F_G, F_S, each
+// replicated once per XCD (a waiting workgroup polls its own XCD's copy: 1/8
+// of the pollers on any line); then the arrival counters of groups of 32
+// items (G_GRP: up to 1024 G items, S_GRP: 128 S items).  Same-address atomics
 // serialize at ~11 ns each, so 246 G items arriving together on one counter
 // took ~2.7 us; a group's last arriver (told by its add's return value) adds
 // once to the phase's top counter instead.
@@ -100,6 +104,21 @@ template <typename V>
 __device__ __forceinline__ V ld1(const V *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16-B sc1 load at byte offset off of a wave-uniform base (buffer_load_dwordx4
+// ... sc1: bypasses L1, served from L2 / memory)
+__device__ __forceinline__ d2v ld1_16(const double *base, unsigned nbytes, unsigned off) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base), 0, nbytes, 0x00020000);
+    return __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
+// 16-B write-through (sc1) store at byte offset off of a wave-uniform base
+// (MI355X_MICROARCH.md: narrow sc1 stores cost ~2.7x per byte)
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st1_16(double *base, unsigned nbytes, unsigned off, d2v v) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, nbytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, off, 0, 16);
+}
+
 // G_ij from the packed upper tiles (u_at) with sc1 loads
 __device__ __forceinline__ double u_at1(const double *U, int T, int r, int c) {
     const int br = r >> 6, bc = c >> 6, ir = r & 63, ic = c & 63;
@@ -241,34 +260,57 @@ struct SmallStage {
     static constexpr int PER = (ROWS * SMALL_GR + 255) / 256;  // 16-B granules per thread
     d2v v[PER];
     // every load of the item in flight at once (coalesced rows)
-    __device__ __forceinline__ void load(const SmallArgs &a, int s) {
+    __device__ __forceinline__ void load(const SmallArgs &a, int s, int tid) {
         const T *X = (const T *)a.X;
         const int64_t c0 = (int64_t)s * SMALL_KC;
         const int len = (int)(c0 + SMALL_KC < a.d ? SMALL_KC : a.d - c0);
+        static_assert(PER * 256 == ROWS * SMALL_GR, "every thread stages PER whole granules");
+        if (VEC && len == SMALL_KC) {  // a full chunk: no per-load guard (no branch per load)
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int gidx = tid + 256 * q;
+                const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
+                v[q] = sm_ld2<T, true>(X + (int64_t)min(row, a.n - 1) * a.ld + c0 + col);
+            }
+            return;
+        }
+        const int len2 = len & ~1;  // the ragged chunk's whole pairs
+        if (VEC && len2 >= 2) {
+            // the ragged last chunk of aligned rows: 16-B loads at clamped
+            // pairs, out-of-range columns zeroed by a select, and for an odd
+            // length its last element by one more load -- no branch per load
+            // (element loads at clamped columns staged this chunk in ~5 us
+            // against ~2 for a full one, and the phase waits for the last)
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int gidx = tid + 256 * q;
+                const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
+                const T *p = X + (int64_t)min(row, a.n - 1) * a.ld + c0;
+                const d2v pr = sm_ld2<T, true>(p + (col < len2 ? col : len2 - 2));
+                const double tl = (double)p[len - 1];
+                v[q] = d2v{col < len2 ? pr.x : (col == len - 1 ? tl : 0.0), col + 1 < len2 ? pr.y : 0.0};
+            }
+            return;
+        }
+        // unaligned rows (or a 1-column chunk): element loads at clamped
+        // columns, out-of-range ones zeroed by a select
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const int gidx = threadIdx.x + 256 * q;
-            const int row = gidx / SMALL_GR, gr = gidx % SMALL_GR, col = 2 * gr;
-            d2v x = {0.0, 0.0};
-            if (row < ROWS) {
-                const T *p = X + (int64_t)min(row, a.n - 1) * a.ld + c0 + col;
-                if (VEC && col + 1 < len) {
-                    x = sm_ld2<T, true>(p);
-                } else {
-                    x.x = col < len ? (double)p[0] : 0.0;
-                    x.y = col + 1 < len ? (double)p[1] : 0.0;
-                }
-            }
-            v[q] = x;
+            const int gidx = tid + 256 * q;
+            const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
+            const T *p = X + (int64_t)min(row, a.n - 1) * a.ld + c0;
+            const double x0 = (double)p[col < len ? col : len - 1];
+            const double x1 = (double)p[col + 1 < len ? col + 1 : len - 1];
+            v[q] = d2v{col < len ? x0 : 0.0, col + 1 < len ? x1 : 0.0};
         }
     }
     // granules [g0, g1) of every row into LDS
-    __device__ __forceinline__ void store(char *tile, int g0, int g1) {
+    __device__ __forceinline__ void store(char *tile, int g0, int g1, int tid) {
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const int gidx = threadIdx.x + 256 * q;
+            const int gidx = tid + 256 * q;
             const int row = gidx / SMALL_GR, gr = gidx % SMALL_GR;
-            if (row < ROWS && gr >= g0 && gr < g1) *reinterpret_cast<d2v *>(tile + sg_off(row, gr)) = v[q];
+            if (gr >= g0 && gr < g1) *reinterpret_cast<d2v *>(tile + sg_off(row, gr)) = v[q];
         }
     }
 };
@@ -295,13 +337,12 @@ __device__ __forceinline__ void small_gram_groups(d4 *acc, const char *tile, int
 // G item (chunk c, part PART): columns [KC c, KC c + KC) staged once, then
 // wave W runs part PART of its blocks b = W + 4 j (the j range cut in SPLIT
 // pieces), so the Gram's MFMAs spread over SPLIT times as many CUs while a
-// chunk's partial (one per KC columns: ~NBLK * 2 KiB written sc1, the same
-// bytes whatever KC is) is written once per KC columns; the partials written
-// sc1.  (Staging half the columns and computing it while the other half
+// chunk's partial (one per KC columns, the same bytes whatever KC is) is
+// written once per KC columns; the partials written sc1.  (Staging half the columns and computing it while the other half
 // landed was 1.3 us slower per item: one more barrier.)
 template <typename T, bool VEC, int NB, int W, int PART>
 __device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int c, long long *tr, int lane,
-                                                char *tile, SmallStage<T, VEC, NB> &st) {
+                                                char *tile, SmallStage<T, VEC, NB> &st, double *wb) {
     constexpr int NBLK = NB * (NB + 1) / 2;
     constexpr int NJ = (NBLK - W + 3) / 4;  // this wave's blocks
     constexpr int J0 = PART * NJ / SMALL_SPLIT, J1 = (PART + 1) * NJ / SMALL_SPLIT;
@@ -310,7 +351,7 @@ __device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int c, long 
     d4 acc[NJ > 0 ? NJ : 1];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
-    st.store(tile, 0, SMALL_GR);
+    st.store(tile, 0, SMALL_GR, lane + 64 * W);
     __syncthreads();
     stamp(tr, 0);
     small_gram_groups<NB, W, J0, J1>(acc, tile, lane, 0, NG);
@@ -318,90 +359,139 @@ __device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int c, long 
         if (tr && J1 > J0) asm volatile("s_nop 0" ::"v"(acc[J0][0]));
         stamp(tr, 1);
     }
+    // the chunk's partial Gram in full-square layout (row-major NP x NP, NP =
+    // 16 NB) plus its diagonal as a contiguous vector, so that an S item reads
+    // its row and every G_jj in coalesced runs.  Each block goes through this
+    // wave's 16 x 17 LDS scratch and out as 16-B sc1 stores: as it is and
+    // transposed for an off-diagonal block; a diagonal block is first made
+    // symmetric from its upper elements (as the packed upper U held them), so
+    // the square is exactly symmetric
+    constexpr int NP = 16 * NB;
+    constexpr unsigned NBYTES = (NP * NP + NP) * 8;
+    double *sq = a.part + (int64_t)__builtin_amdgcn_readfirstlane(c) * (NP * NP + NP);
 #pragma unroll
     for (int j = J0; j < J1; ++j) {
-        double *out = a.part + ((int64_t)c * NBLK + W + 4 * j) * 256;
+        const int b = W + 4 * j;
+        const int bi = blk_bi(b, NB), bj = blk_bj(b, NB);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) st1(out + (g + 4 * r) * 16 + rr, (double)acc[j][r]);
+        for (int r = 0; r < 4; ++r) wb[(g + 4 * r) * 17 + rr] = (double)acc[j][r];
+        if (bi == bj) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (g + 4 * r > rr) wb[(g + 4 * r) * 17 + rr] = wb[rr * 17 + g + 4 * r];
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int gi = lane + 64 * q, row = gi >> 3, gc = gi & 7;
+            st1_16(sq, NBYTES, ((16 * bi + row) * NP + 16 * bj + 2 * gc) * 8,
+                   d2v{wb[row * 17 + 2 * gc], wb[row * 17 + 2 * gc + 1]});
+            if (bi != bj)
+                st1_16(sq, NBYTES, ((16 * bj + row) * NP + 16 * bi + 2 * gc) * 8,
+                       d2v{wb[(2 * gc) * 17 + row], wb[(2 * gc + 1) * 17 + row]});
+        }
+        if (bi == bj && lane < 8)
+            st1_16(sq, NBYTES, (NP * NP + 16 * bi + 2 * lane) * 8,
+                   d2v{wb[(2 * lane) * 17 + 2 * lane], wb[(2 * lane + 1) * 17 + 2 * lane + 1]});
     }
 }
 
 template <typename T, bool VEC, int NB, int W>
 __device__ __forceinline__ void small_gram_w(const SmallArgs &a, int c, int h, long long *tr,
-                                             int lane, char *tile, SmallStage<T, VEC, NB> &st) {
+                                             int lane, char *tile, SmallStage<T, VEC, NB> &st,
+                                             double *wb) {
     static_assert(SMALL_SPLIT == 4, "parts");
     switch (h) {
-    case 0: small_gram_wave<T, VEC, NB, W, 0>(a, c, tr, lane, tile, st); break;
-    case 1: small_gram_wave<T, VEC, NB, W, 1>(a, c, tr, lane, tile, st); break;
-    case 2: small_gram_wave<T, VEC, NB, W, 2>(a, c, tr, lane, tile, st); break;
-    default: small_gram_wave<T, VEC, NB, W, 3>(a, c, tr, lane, tile, st); break;
+    case 0: small_gram_wave<T, VEC, NB, W, 0>(a, c, tr, lane, tile, st, wb); break;
+    case 1: small_gram_wave<T, VEC, NB, W, 1>(a, c, tr, lane, tile, st, wb); break;
+    case 2: small_gram_wave<T, VEC, NB, W, 2>(a, c, tr, lane, tile, st, wb); break;
+    default: small_gram_wave<T, VEC, NB, W, 3>(a, c, tr, lane, tile, st, wb); break;
     }
 }
 
 template <typename T, bool VEC, int NB>
 __device__ __forceinline__ void small_gram(const SmallArgs &a, int it, int wave, int lane,
-                                           char *tile) {
+                                           char *tile, double *wb) {
     int c, h;
     g_item(it, a.P, c, h);
     long long *tr = a.trace ? a.trace + 8 * (int64_t)it : nullptr;
     SmallStage<T, VEC, NB> st;
-    st.load(a, c);
+    st.load(a, c, lane + 64 * wave);
     switch (wave) {
-    case 0: small_gram_w<T, VEC, NB, 0>(a, c, h, tr, lane, tile, st); break;
-    case 1: small_gram_w<T, VEC, NB, 1>(a, c, h, tr, lane, tile, st); break;
-    case 2: small_gram_w<T, VEC, NB, 2>(a, c, h, tr, lane, tile, st); break;
-    default: small_gram_w<T, VEC, NB, 3>(a, c, h, tr, lane, tile, st); break;
+    case 0: small_gram_w<T, VEC, NB, 0>(a, c, h, tr, lane, tile, st, wb); break;
+    case 1: small_gram_w<T, VEC, NB, 1>(a, c, h, tr, lane, tile, st, wb); break;
+    case 2: small_gram_w<T, VEC, NB, 2>(a, c, h, tr, lane, tile, st, wb); break;
+    default: small_gram_w<T, VEC, NB, 3>(a, c, h, tr, lane, tile, st, wb); break;
     }
 }
 
-// R item q: 64 elements (quarter q & 3) of block q >> 2, summed over the P
-// partials in a fixed order (4 interleaved chains, then the chains in order)
-__device__ __forceinline__ void small_reduce(const SmallArgs &a, int q, int tid, int NB,
-                                             double (*red)[64]) {
-    const int b = q >> 2, h = q & 3, el = tid & 63, ch = tid >> 6;
-    const int e = 64 * h + el;
-    const double *p = a.part + (int64_t)b * 256 + e;
-    const int64_t stride = (int64_t)a.nblk * 256;
-    double acc = 0.0;
-    int s = ch;
-    for (; s < a.P; s += 4 * 32) {  // 32 loads in flight per thread (P <= 512: 4 rounds at most)
-        double v[32];
-#pragma unroll
-        for (int u = 0; u < 32; ++u) v[u] = s + 4 * u < a.P ? ld1(p + (int64_t)(s + 4 * u) * stride) : 0.0;
-#pragma unroll
-        for (int u = 0; u < 32; ++u)
-            if (s + 4 * u < a.P) acc += v[u];
-    }
-    red[ch][el] = acc;
-    __syncthreads();
-    if (ch == 0) {
-        const double t = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
-        const int bi = blk_bi(b, NB), bj = blk_bj(b, NB);
-        const int r = 16 * bi + (e >> 4), c = 16 * bj + (e & 15);
-        st1(a.U + upper_tile(a.T, r >> 6, c >> 6) + (r & 63) * 64 + (c & 63), t);
-        if (q == 0 && el == 0) st1(a.U + (int64_t)a.T * (a.T + 1) / 2 * 4096, (double)a.d);
-    }
+// upper 16x16 block index of block (bi <= bj) in an NB x NB grid (row-major)
+__device__ __forceinline__ int blk_idx(int bi, int bj, int NB) {
+    return bi * NB - bi * (bi - 1) / 2 + (bj - bi);
 }
 
-// S item i: row i with the whole workgroup.  Distances, then a sort by
+// S item i: row i with the whole workgroup, straight from the G items'
+// full-square partials (no separate reduce phase): G_ij (the upper element
+// (min, max), as the packed upper U held it) and every G_jj, each summed over
+// the P chunk partials in chunk order.  Then the distances, a sort by
 // counting (thread t ranks key t & 127 against half of the row, t >> 7; key e
-// goes to position #{keys before it in the (value, index) total order}), then
+// goes to position #{keys before it in the (value, index) total order}), and
 // K2's summation with its own 256 threads: thread t sums rank 1 + t, the wave
-// butterfly, the 4 waves in order -- the same sorted array and the same shape,
-// so the score is K2's bitwise (for the same U).
+// butterfly, the 4 waves in order -- the same sorted array and the same
+// shape, so the score is K2's bitwise for the same Gram.
+template <int NB>
 __device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid, uint64_t *kbuf,
-                                             double *sbuf, int *rk, double *red, long long *tr) {
+                                             double *sbuf, int *rk, double *gv, d2v *gv2,
+                                             double *red, long long *tr) {
     const int n = a.n, lane = tid & 63, wave = tid >> 6;
     const int64_t k = n - a.f - 2 > 0 ? n - a.f - 2 : 0;
-    const int e = tid & 127, h = tid >> 7;
-    const double di = u_at1(a.U, a.T, i, i);
-    if (h == 0) {
-        uint64_t key = ~0ULL;  // padding sorts last
-        if (e < n) key = dkey((di + u_at1(a.U, a.T, e, e)) - 2.0 * u_at1(a.U, a.T, i, e));
-        kbuf[e] = key;
+    // 16-B element pairs of the row (NP/2) and of the diagonal vector (NP/2),
+    // each summed over the P chunk partials in two fixed chains (chunks
+    // [0, P/2) and [P/2, P), each in order), then chain 0 + chain 1; a
+    // wave's lanes read consecutive 16-B granules (sc1 16-B loads move ~1.5x
+    // the bytes per second of 8-B ones)
+    const int NP = 16 * NB;
+    const int64_t stride = (int64_t)NP * NP + NP;
+    const int pr = tid % NP, ch = tid / NP;  // pair pr < NP (row: pr < NP/2), chain ch < 256/NP
+    const int half = (a.P + 1) >> 1;
+    if (ch < 2) {
+        const unsigned e0 = pr < NP / 2 ? (unsigned)(i * NP + 2 * pr) : (unsigned)(NP * NP + 2 * pr - NP);
+        const unsigned nbytes = (unsigned)(a.P * stride * 8);
+        const int sb = ch ? half : 0, se = ch ? a.P : half;
+        d2v acc = {0.0, 0.0};
+        for (int s0 = sb; s0 < se; s0 += 32) {  // P <= 256: 4 rounds at most
+            d2v v[32];
+            // every load unconditional (past the chain's end: its last chunk
+            // again, dropped below), so no branch per load; acc starts at
+            // +0.0 and is never -0.0, so adding +0.0 leaves it bit for bit
+#pragma unroll
+            for (int u = 0; u < 32; ++u)
+                v[u] = ld1_16(a.part, nbytes, (unsigned)((e0 + (s0 + u < se ? s0 + u : se - 1) * stride) * 8));
+#pragma unroll
+            for (int u = 0; u < 32; ++u) {
+                const bool on = s0 + u < se;
+                acc.x += on ? v[u].x : 0.0;
+                acc.y += on ? v[u].y : 0.0;
+            }
+        }
+        gv2[ch * NP + pr] = acc;
+    }
+    __syncthreads();
+    // gv[j] = G_ij (j < NP), gv[NP + j] = G_jj
+    if (tid < NP) {
+        const d2v c0 = gv2[tid], c1 = gv2[NP + tid];
+        gv[2 * tid] = c0.x + c1.x;
+        gv[2 * tid + 1] = c0.y + c1.y;
     }
     __syncthreads();
     stamp(tr, 0);
+    const int e = tid & 127, h = tid >> 7;
+    const double di = gv[NP + i];
+    if (h == 0) {
+        uint64_t key = ~0ULL;  // padding sorts last
+        if (e < n) key = dkey((di + gv[NP + e]) - 2.0 * gv[e]);
+        kbuf[e] = key;
+    }
+    __syncthreads();
     const uint64_t key = kbuf[e];
     int cnt = 0;
 #pragma unroll
@@ -435,44 +525,65 @@ __device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid,
     }
 }
 
-// M item c: every M item ranks the n published scores itself (n <= 128: one
-// LDS pass, no separate selection hand-off), compacts the selection with
-// ballots, and sums columns [128 c, 128 c + 128) of the m selected rows in
-// ascending order (K4's order: the same bits), every load in flight at once.
-// Item 0 also writes sel and the margin.
-template <typename T>
-__device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int wave, int lane,
-                                           uint64_t *keys, int64_t *soff, double *dg, double *bnd,
-                                           uint64_t *balw, int *rkm, char *tile, long long *tr) {
-    const int n = a.n, m = n - a.f, tid = threadIdx.x;
+// M item c, part 1 (before the scores exist): columns [64 c, 64 c + 64) of
+// every row into LDS as fp64 (exact for fp32 rows), every load in flight --
+// so after the scores only LDS work is left.  Thread t: column t & 63, rows
+// t >> 6, + 4, ...
+template <typename T, int NB>
+__device__ __forceinline__ void small_mean_stage(const SmallArgs &a, int c, int tid, double *cols) {
+    if (!a.mean) return;
+    const int cl = tid & 63, r0 = tid >> 6;
+    const int64_t col = (int64_t)c * 64 + cl;
+    const T *X = (const T *)a.X + (col < a.d ? col : a.d - 1);
+    // rows r0, r0 + 4, ... < 16 NB (rows past n repeat row n - 1: loads
+    // without a guard, and the mean's mask never selects them)
+    double v[4 * NB];
+#pragma unroll
+    for (int u = 0; u < 4 * NB; ++u) {
+        const int r = r0 + 4 * u;
+        v[u] = (double)X[(int64_t)(r < a.n ? r : a.n - 1) * a.ld];
+    }
+#pragma unroll
+    for (int u = 0; u < 4 * NB; ++u) cols[(r0 + 4 * u) * 64 + cl] = v[u];
+}
+
+// M item c, part 2: every M item ranks the n published scores itself (n <=
+// 128: one LDS pass, no separate selection hand-off), compacts the selection
+// with ballots, and sums its 64 staged columns of the m selected rows in
+// ascending order from LDS (K4's order: the same bits).  Item 0 also writes
+// sel and the margin.
+template <int NB>
+__device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int tid, int wave, int lane,
+                                           uint64_t *keys, int *srow, double *dg, double *bnd,
+                                           uint64_t *balw, int *rkm, const double *cols,
+                                           long long *tr) {
+    const int n = a.n, m = n - a.f;
     double si = 0.0;
     if (tid < n) {
         si = ld1(a.scores + tid);
         keys[tid] = dkey(si);
-    } else if (c == 0 && tid >= 128 && tid - 128 < n) {
+    } else if (tid < 128) {
+        keys[tid] = ~0ULL;  // padding: after every real key (NaN included)
+    } else if (c == 0 && tid - 128 < n) {
         dg[tid - 128] = ld1(a.diag + tid - 128);
     }
     __syncthreads();
     stamp(tr, 0);
     // rank of row e in the (score, index) total order: threads e and 128 + e
-    // count over the two halves of the keys
+    // count over the two halves of the 128 (padded) keys -- a fixed trip
+    // count, every LDS read issued ahead, no branch
     const int e = tid & 127, h = tid >> 7;
+    const uint64_t ki = keys[e];
     int cnt = 0;
-    uint64_t ki = 0;
-    if (e < n) {
-        ki = keys[e];
-        const int j1 = n < 64 * h + 64 ? n : 64 * h + 64;
-        int j = 64 * h;
-        for (; j + 8 <= j1; j += 8) {
-            uint64_t o[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) o[u] = keys[j + u];
+    for (int j0 = 0; j0 < 64; j0 += 8) {
+        uint64_t o[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) cnt += (o[u] < ki) || (o[u] == ki && j + u < e);
-        }
-        for (; j < j1; ++j) {
-            const uint64_t o = keys[j];
-            cnt += (o < ki) || (o == ki && j < e);
+        for (int u = 0; u < 8; ++u) o[u] = keys[64 * h + j0 + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = 64 * h + j0 + u;
+            cnt += (o[u] < ki) || (o[u] == ki && j < e);
         }
     }
     if (h == 1 && e < n) rkm[e] = cnt;
@@ -490,7 +601,7 @@ __device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int wave, 
     __syncthreads();
     if (on) {
         const int pos = (wave ? __popcll(balw[0]) : 0) + __popcll(bal & ((1ull << lane) - 1));
-        soff[pos] = (int64_t)tid * a.ld;
+        srow[pos] = tid;
         if (c == 0 && a.sel) a.sel[pos] = (int64_t)tid;
     }
     if (c == 0 && wave == 3) {
@@ -512,60 +623,32 @@ __device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int wave, 
     }
     __syncthreads();
     stamp(tr, 1);
-    if (!a.mean) return;
-    // the selected rows' offsets in registers (lane u: selected row u, or
-    // 64 + u in waves 2-3; lanes past m repeat row m - 1, so every load is
-    // valid), read with v_readlane per load instead of a broadcast LDS read +
-    // wait per load.  v_readlane ignores EXEC, so no lane may skip the offset
-    // loads: every lane runs the loads (columns past d clamped to the last one)
-    // and only the store is conditional.  mm (= m) is re-derived from LDS so
-    // the per-row tests stay inside the item (hoisted out of the item loop,
-    // 64 loop-invariant masks were spilled and cost ~4 us per item).
-    // Waves 0-1 load rows 0..63 of the item's 128 columns, waves 2-3 rows
-    // 64..m-1 at the same time into LDS (the G tile: (m - 64) KiB <= 8 NB KiB);
-    // waves 0-1 then add them in order: K4's ascending sum, bit for bit
-    const int mm = __popcll(balw[0]) + __popcll(balw[1]);
-    const int cl = e;  // (e = tid & 127, h = tid >> 7 as in the rank)
-    const int64_t col = (int64_t)c * 128 + cl;
-    const T *X = (const T *)a.X + (col < a.d ? col : a.d - 1);
-    double *spill = reinterpret_cast<double *>(tile);  // [row - 64][128]
-    const int64_t o = soff[64 * h + lane < mm ? 64 * h + lane : mm - 1];
+    if (!a.mean || wave != 0) return;
+    // one column per lane of wave 0: the 16 NB staged rows in ascending order
+    // from LDS (immediate-offset reads, no index chain, no branch), each
+    // row's value or +0.0 by the selection mask.  acc starts at +0.0 and a round-to-nearest sum is
+    // -0.0 only if both addends are, so acc is never -0.0 and acc + 0.0 == acc
+    // bit for bit (NaN and inf included): the adds of the selected rows in
+    // ascending order, K4's sum, bit for bit
+    const int64_t col = (int64_t)c * 64 + lane;
+    // the selection masks in SGPRs (bit r: row r, resp. 64 + r, selected;
+    // zero past n), so each row's select is a scalar test
+    const uint64_t s0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(balw[0] >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)balw[0]);
+    const uint64_t s1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(balw[1] >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)balw[1]);
     double acc = 0.0;
-    if (h == 0) {
-        double v[64];
 #pragma unroll
-        for (int u = 0; u < 64; ++u) v[u] = (double)X[__builtin_amdgcn_readlane((long long)o, u)];
-#pragma unroll
-        for (int u = 0; u < 64; ++u) acc = u < mm ? acc + v[u] : acc;
-    } else if (mm > 64) {
-        double v[64];
-#pragma unroll
-        for (int u = 0; u < 64; ++u) v[u] = (double)X[__builtin_amdgcn_readlane((long long)o, u)];
-#pragma unroll
-        for (int u = 0; u < 64; ++u)
-            if (64 + u < mm) spill[u * 128 + cl] = v[u];
+    for (int r = 0; r < (NB < 4 ? 16 * NB : 64); ++r) {
+        const double v = cols[r * 64 + lane];
+        acc += ((s0 >> r) & 1) ? v : 0.0;
     }
-    __syncthreads();
-    if (h == 0) {
-        for (int u = 64; u < mm; ++u) acc += spill[(u - 64) * 128 + cl];
-        if (col < a.d) a.mean[col] = acc / (double)m;
-    }
-}
-
-template <typename T>
-__device__ __forceinline__ void small_prefetch(const SmallArgs &a, int c, int tid) {
-    const int64_t col = (int64_t)c * 128 + (tid & 127);
-    if (!a.mean || col >= a.d) return;
-    const T *X = (const T *)a.X;
-    T acc = 0;
-    for (int r = tid >> 7; r < a.n; r += 32) {
-        T v[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = r + 2 * u < a.n ? X[(int64_t)(r + 2 * u) * a.ld + col] : (T)0;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) acc += v[u];
+    for (int r = 0; r < 16 * NB - 64; ++r) {
+        const double v = cols[(64 + r) * 64 + lane];
+        acc += ((s1 >> r) & 1) ? v : 0.0;
     }
-    asm volatile("" ::"v"(acc));  // keep the loads
+    if (col < a.d) a.mean[col] = acc / (double)m;
 }
 
 template <typename T, bool VEC, int NB>
@@ -576,20 +659,24 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     __shared__ uint64_t kbuf[128];                                      // S / selection keys
     __shared__ __attribute__((aligned(16))) double sbuf[128];          // S: the sorted row
     __shared__ int rk[128];
-    __shared__ double red[4][64];                                       // R chains, S waves
+    __shared__ double red[4];                                           // S waves
     __shared__ double bnd[2];
     __shared__ double dgl[128];
-    __shared__ int64_t soff[128];
+    __shared__ int srow[128];
     __shared__ uint64_t balw[2];
+    __shared__ double wbuf[4][16 * 17];  // G: each wave's block on its way out
+    static_assert(16 * NB * SMALL_GR * 16 >= 6 * 16 * NB * 8, "S items keep their sums in the tile");
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int NGI = SMALL_SPLIT * a.P;  // G items: SPLIT per chunk
-    const int total = NGI + a.Q + a.n + a.C;
+    const int total = NGI + a.n + a.C;
     unsigned *ctr = a.ctr;
     // the first S0 items (G items) go to workgroups by blockIdx, the rest in
     // queue order (one returning atomic each): 256 dequeues on one counter
     // take ~3 us, which delayed the last G item's start by that much
     const int S0 = NGI < (int)gridDim.x ? NGI : (int)gridDim.x;
     bool last_out = false;
+    // debug trace: per workgroup {entry, exit} after the item records
+    if (a.trace && tid == 0) a.trace[8 * total + 2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
     for (bool first = true;; first = false) {
         if (first && (int)blockIdx.x < S0) {
             if (tid == 0) s_item = (int)blockIdx.x;
@@ -599,6 +686,17 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
         }
         __syncthreads();
         const int it = s_item;
+        // the item's view of the arguments, opaque to the optimizer: without
+        // this, every predicate and constant the items derive from n, f, P, d
+        // (row masks, chunk masks, the margin's gamma divisions) was hoisted
+        // out of the item loop into a ~2,300-instruction prologue, spilled to
+        // VGPR lanes and run cold from the instruction cache: 4.4 us before
+        // the first item started
+        SmallArgs b = a;
+        asm volatile("" : "+s"(b.n), "+s"(b.f), "+s"(b.P), "+s"(b.C), "+s"(b.d), "+s"(b.ld));
+        int ot = tid;  // the thread index, opaque likewise (per-thread LDS / row offsets)
+        asm volatile("" : "+v"(ot));
+        const int olane = ot & 63;
         __syncthreads();
         if (it >= total) {
             // every workgroup ends on exactly one failed dequeue; the last of
@@ -612,27 +710,26 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
             m0 = (long long)__builtin_amdgcn_s_memtime();
         }
         if (it < NGI) {
-            small_gram<T, VEC, NB>(a, it, wave, lane, tile);
+            small_gram<T, VEC, NB>(b, it, wave, olane, tile, &wbuf[wave][0]);
             if (wg_arrive(ctr, C_G, G_GRP, it, NGI, &s_old)) wg_raise(ctr, F_G);
-        } else if (it < NGI + a.Q) {
+        } else if (it < NGI + a.n) {
             wg_wait_flag(ctr, F_G);
             if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-            small_reduce(a, it - NGI, tid, NB, red);
-            if (wg_arrive(ctr, C_R, R_GRP, it - NGI, a.Q, &s_old)) wg_raise(ctr, F_R);
-        } else if (it < NGI + a.Q + a.n) {
-            wg_wait_flag(ctr, F_R);
-            if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-            small_scores(a, it - NGI - a.Q, tid, kbuf, sbuf, rk, &red[0][0],
+            // the S item's chain sums and Gram row live in the (idle) G tile
+            d2v *gv2 = reinterpret_cast<d2v *>(tile);
+            double *gv = reinterpret_cast<double *>(tile) + 4 * 16 * NB;
+            small_scores<NB>(b, it - NGI, ot, kbuf, sbuf, rk, gv, gv2, red,
                          a.trace ? a.trace + 8 * it : nullptr);
-            if (wg_arrive(ctr, C_S, S_GRP, it - NGI - a.Q, a.n, &s_old)) wg_raise(ctr, F_S);
+            if (wg_arrive(ctr, C_S, S_GRP, it - NGI, a.n, &s_old)) wg_raise(ctr, F_S);
         } else {
-            // while the scores are computed: pull this item's columns of
-            // every row toward this XCD's L2, so the mean's loads hit it
-            small_prefetch<T>(a, it - NGI - a.Q - a.n, tid);
+            // while the scores are computed: this item's 64 columns of every
+            // row into LDS, so after the scores only LDS work is left
+            double *cols = reinterpret_cast<double *>(tile);
+            small_mean_stage<T, NB>(b, it - NGI - a.n, ot, cols);
             wg_wait_flag(ctr, F_S);
             if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-            small_mean<T>(a, it - NGI - a.Q - a.n, wave, lane, kbuf, soff, dgl, bnd, balw, rk, tile,
-                          a.trace ? a.trace + 8 * it : nullptr);
+            small_mean<NB>(b, it - NGI - a.n, ot, wave, olane, kbuf, srow, dgl, bnd, balw, rk, cols,
+                       a.trace ? a.trace + 8 * it : nullptr);
         }
         if (a.trace && tid == 0) {
             unsigned hw;
@@ -653,9 +750,10 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
             a.margin[2] = 2.0;  // read_margin reports BK_EHIP
         }
         __syncthreads();
-        for (int w = tid; w < C_LINES * 32; w += 256)
-            __hip_atomic_store(ctr + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // only word 0 of each line is ever written
+        if (tid < C_LINES) __hip_atomic_store(ctr + 32 * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (a.trace && tid == 0) a.trace[8 * total + 2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 template <typename T, bool VEC>
@@ -681,9 +779,9 @@ SmallPlan small_plan(int n, int64_t d, int num_cu) {
     p.kc = (int)kc;
     p.P = (int)((d + kc - 1) / kc);
     p.ng = SMALL_SPLIT * p.P;
-    p.Q = 4 * p.nblk;
+    p.Q = 0;   // no reduce items: every S item sums its own row of the partials
     p.nS = n;  // one S item per row
-    p.C = (int)((d + 127) / 128);
+    p.C = (int)((d + 63) / 64);  // M items: 64 columns each
     return p;
 }
 
@@ -713,7 +811,7 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     a.margin = margin;
     a.sel = sel;
     a.ctr = ctr;
-    const int total = SMALL_SPLIT * a.P + a.Q + a.n + a.C;
+    const int total = SMALL_SPLIT * a.P + a.n + a.C;
     const int grid = total < num_cu ? total : num_cu;
     const bool vec = (ld % 2) == 0 && ((uintptr_t)X % (dtype == 0 ? 16 : 8)) == 0;
     if (dtype == 0 && vec)

@@ -29,11 +29,12 @@ if sys.argv[1] == "run":
 raw = np.fromfile(sys.argv[1], dtype=np.int64)
 pos, calls = 0, []
 while pos < len(raw):
-    items, P, Q, nS, C = raw[pos:pos + 5]
-    tr = raw[pos + 5:pos + 5 + 8 * items].reshape(items, 8)
-    calls.append((P, Q, nS, C, tr))
-    pos += 5 + 8 * items
-P, Q, nS, C, tr = calls[-1]
+    items, P, Q, nS, C, grid = raw[pos:pos + 6]
+    tr = raw[pos + 6:pos + 6 + 8 * items].reshape(items, 8)
+    wg = raw[pos + 6 + 8 * items:pos + 6 + 8 * items + 2 * grid].reshape(grid, 2)
+    calls.append((P, Q, nS, C, tr, wg))
+    pos += 6 + 8 * items + 2 * grid
+P, Q, nS, C, tr, wg = calls[-1]
 t0 = tr[:, 0][tr[:, 0] > 0].min()
 us = lambda x: (x - t0) / 100.0  # s_memrealtime: 100 MHz
 kinds = [("G", 0, P), ("R", P, P + Q), ("S", P + Q, P + Q + nS), ("M", P + Q + nS, P + Q + nS + C)]
@@ -53,3 +54,5 @@ for name, a, b in kinds:
 clk = (tr[:, 5] - tr[:, 4]) / np.maximum(1, tr[:, 2] - tr[:, 0]) * 100 / 1000.0
 print("shader clock (GHz) over items: median %.2f min %.2f" % (np.median(clk[clk > 0]), clk[clk > 0].min()))
 print("calls traced: %d; last call span %.2f us" % (len(calls), us(tr[:, 2]).max()))
+print("workgroups %d: entry %.2f..%.2f us (first item at 0), exit %.2f..%.2f us"
+      % (len(wg), us(wg[:, 0]).min(), us(wg[:, 0]).max(), us(wg[:, 1]).min(), us(wg[:, 1]).max()))
