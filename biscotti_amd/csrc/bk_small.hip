@@ -265,30 +265,29 @@ struct SmallStage {
         const int64_t c0 = (int64_t)s * SMALL_KC;
         const int len = (int)(c0 + SMALL_KC < a.d ? SMALL_KC : a.d - c0);
         static_assert(PER * 256 == ROWS * SMALL_GR, "every thread stages PER whole granules");
-        if (VEC && len == SMALL_KC) {  // a full chunk: no per-load guard (no branch per load)
-#pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                const int gidx = tid + 256 * q;
-                const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
-                v[q] = sm_ld2<T, true>(X + (int64_t)min(row, a.n - 1) * a.ld + c0 + col);
-            }
-            return;
-        }
-        const int len2 = len & ~1;  // the ragged chunk's whole pairs
+        const int len2 = len & ~1;  // whole column pairs of this chunk (KC but for the last)
         if (VEC && len2 >= 2) {
-            // the ragged last chunk of aligned rows: 16-B loads at clamped
-            // pairs, out-of-range columns zeroed by a select, and for an odd
-            // length its last element by one more load -- no branch per load
-            // (element loads at clamped columns staged this chunk in ~5 us
-            // against ~2 for a full one, and the phase waits for the last)
+            // ONE code path for full chunks and the ragged last one: 16-B loads
+            // at clamped pairs, columns past the chunk zeroed by a select, no
+            // branch per load.  A separate path for the ragged chunk ran its
+            // items ~3-5 us behind the others (its code ran cold from the
+            // instruction cache on the few CUs that took it), and the phase
+            // waits for the last item
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
                 const int gidx = tid + 256 * q;
                 const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
                 const T *p = X + (int64_t)min(row, a.n - 1) * a.ld + c0;
                 const d2v pr = sm_ld2<T, true>(p + (col < len2 ? col : len2 - 2));
-                const double tl = (double)p[len - 1];
-                v[q] = d2v{col < len2 ? pr.x : (col == len - 1 ? tl : 0.0), col + 1 < len2 ? pr.y : 0.0};
+                v[q] = d2v{col < len2 ? pr.x : 0.0, col + 1 < len2 ? pr.y : 0.0};
+            }
+            if (len & 1) {  // an odd ragged chunk: its last column (rare)
+#pragma unroll
+                for (int q = 0; q < PER; ++q) {
+                    const int gidx = tid + 256 * q;
+                    const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
+                    if (col == len - 1) v[q].x = (double)X[(int64_t)min(row, a.n - 1) * a.ld + c0 + col];
+                }
             }
             return;
         }
