@@ -665,7 +665,7 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     __shared__ uint64_t balw[2];
     __shared__ double wbuf[4][16 * 17];  // G: each wave's block on its way out
     static_assert(16 * NB * SMALL_GR * 16 >= 6 * 16 * NB * 8, "S items keep their sums in the tile");
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, wave = tid >> 6;
     const int NGI = SMALL_SPLIT * a.P;  // G items: SPLIT per chunk
     const int total = NGI + a.n + a.C;
     unsigned *ctr = a.ctr;
