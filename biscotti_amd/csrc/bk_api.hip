@@ -84,6 +84,7 @@ struct bk_ctx {
     // k_small (n <= 128, one launch): its queue counters (zeroed once; every
     // launch leaves them zero) and the split-K partials
     DevBuf small_ctr, small_part;
+    DevBuf mean_part;  // K4 of a large selection: per-segment column sums (launch_mean)
     int small_on = 1;
     int margin_valid = 0;
     // BK_F32_CERTIFIED: 1 while the exact re-run of a near-tie call is in progress
@@ -179,7 +180,8 @@ void bind_epoch(bk_ctx *c) {
     DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,   &c->scores, &c->mask,   &c->sel,
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                      &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part};
+                      &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
+                      &c->mean_part};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -425,10 +427,16 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
                               (double *)c->margin.p, c->stream);
     }));
     c->margin_valid = 1;
-    if (d_mean && d > 0)
+    if (d_mean && d > 0) {
+        double *seg = nullptr;
+        if (mean_segments((int)m) > 1) {
+            CHK(ensure(c->mean_part, (size_t)mean_segments((int)m) * (size_t)d * sizeof(double)));
+            seg = (double *)c->mean_part.p;
+        }
         CHK(timed(c, BK_K_MEAN, [&] {
-            return launch_mean(dX, dtype, ld, d, d_sel, (int)m, d_mean, c->num_cu, c->stream);
+            return launch_mean(dX, dtype, ld, d, d_sel, (int)m, d_mean, c->num_cu, c->stream, seg);
         }));
+    }
     return BK_OK;
 }
 
@@ -766,7 +774,8 @@ void bk_destroy(bk_ctx *c) {
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->scores,
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                          &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part};
+                          &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
+                          &c->mean_part};
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);

@@ -99,8 +99,13 @@ hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bn
 hipError_t launch_compact(const int *mask, int n, int64_t *sel, const double *diag,
                           const double *bnd, const double *dcols, int64_t k, double u_gram,
                           double *margin, hipStream_t st);
+// K4 of a large selection (m >= MEAN_SEG_MIN) sums the selected rows in
+// segments of MEAN_SEG_ROWS (seg_part: mean_segments(m) * d doubles), then
+// the segments in order; the order depends on m only
+constexpr int MEAN_SEG_MIN = 1024, MEAN_SEG_ROWS = 256;
+inline int mean_segments(int m) { return m >= MEAN_SEG_MIN ? (m + MEAN_SEG_ROWS - 1) / MEAN_SEG_ROWS : 1; }
 hipError_t launch_mean(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel, int m,
-                       double *mean, int num_cu, hipStream_t st);
+                       double *mean, int num_cu, hipStream_t st, double *seg_part = nullptr);
 // global[c] += X[idx[0]][c] + X[idx[1]][c] + ... (sequential, idx order)
 hipError_t launch_accumulate(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *idx,
                              int m, double *global, int num_cu, hipStream_t st);

@@ -1472,14 +1472,24 @@ __global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, 
 // ACCUM = false: mean[c] = (sum over r in sel order of X[sel[r]][c]) / m   (K4)
 // ACCUM = true:  mean[c] = mean[c] + X[sel[0]][c] + X[sel[1]][c] + ...       (in sel
 //                order, sequential: the GlobalW update of honest.go:361-375)
-template <typename T, bool VEC, bool ACCUM = false>
+// SEG (a large selection, m >= MEAN_SEG_MIN): block row y sums the selected
+// rows [y L, y L + L) into part[y][c] (no divide), k_mean_comb adds the
+// segments in order -- a fixed order that depends on m only, so every shard
+// and device of one call adds alike
+template <typename T, bool VEC, bool ACCUM = false, bool SEG = false>
 __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t ld, int64_t d,
                                               const int64_t *__restrict__ sel, int m,
                                               double *__restrict__ mean) {
     extern __shared__ __attribute__((aligned(16))) int64_t srow[];  // row offsets (elements)
+    if constexpr (SEG) {
+        const int r0 = (int)blockIdx.y * MEAN_SEG_ROWS;
+        sel += r0;
+        m = m - r0 < MEAN_SEG_ROWS ? m - r0 : MEAN_SEG_ROWS;
+        mean += (int64_t)blockIdx.y * d;
+    }
     for (int r = threadIdx.x; r < m; r += 256) srow[r] = sel[r] * ld;
     __syncthreads();
-    const double dm = (double)m;
+    const double dm = SEG ? 1.0 : (double)m;
     const int64_t npair = (d + 1) >> 1;
     for (int64_t cp = (int64_t)blockIdx.x * 256 + threadIdx.x; cp < npair;
          cp += (int64_t)gridDim.x * 256) {
@@ -1503,7 +1513,7 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
                 acc.x += v.x;
                 acc.y += v.y;
             }
-            if constexpr (ACCUM) {
+            if constexpr (ACCUM || SEG) {
                 mean[c] = acc.x;
                 mean[c + 1] = acc.y;
             } else {
@@ -1513,7 +1523,7 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
         } else {
             double acc = ACCUM ? mean[c] : 0.0;
             for (int r = 0; r < m; ++r) acc += (double)X[srow[r] + c];
-            mean[c] = ACCUM ? acc : acc / dm;
+            mean[c] = (ACCUM || SEG) ? acc : acc / dm;
         }
     }
 }
@@ -1521,14 +1531,20 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
 // fp32 rows with 16-B aligned starts: 4 columns per thread from one 16-B load
 // (the f2v form above moves 8 B per load: config E's K4 ran at 3.9 TB/s).  The
 // same per-column order of adds as k_mean, so the same bits.
-template <bool ACCUM>
+template <bool ACCUM, bool SEG = false>
 __global__ __launch_bounds__(256) void k_mean_f4(const float *__restrict__ X, int64_t ld, int64_t d,
                                                  const int64_t *__restrict__ sel, int m,
                                                  double *__restrict__ mean) {
     extern __shared__ __attribute__((aligned(16))) int64_t srow[];
+    if constexpr (SEG) {  // as k_mean's SEG
+        const int r0 = (int)blockIdx.y * MEAN_SEG_ROWS;
+        sel += r0;
+        m = m - r0 < MEAN_SEG_ROWS ? m - r0 : MEAN_SEG_ROWS;
+        mean += (int64_t)blockIdx.y * d;
+    }
     for (int r = threadIdx.x; r < m; r += 256) srow[r] = sel[r] * ld;
     __syncthreads();
-    const double dm = (double)m;
+    const double dm = SEG ? 1.0 : (double)m;
     const int64_t nq = (d + 3) >> 2;
     for (int64_t cq = (int64_t)blockIdx.x * 256 + threadIdx.x; cq < nq;
          cq += (int64_t)gridDim.x * 256) {
@@ -1554,14 +1570,25 @@ __global__ __launch_bounds__(256) void k_mean_f4(const float *__restrict__ X, in
                 for (int e = 0; e < 4; ++e) acc[e] += (double)v[e];
             }
 #pragma unroll
-            for (int e = 0; e < 4; ++e) mean[c + e] = ACCUM ? acc[e] : acc[e] / dm;
+            for (int e = 0; e < 4; ++e) mean[c + e] = (ACCUM || SEG) ? acc[e] : acc[e] / dm;
         } else {
             for (int64_t cc = c; cc < d; ++cc) {
                 double acc = ACCUM ? mean[cc] : 0.0;
                 for (int r = 0; r < m; ++r) acc += (double)X[srow[r] + cc];
-                mean[cc] = ACCUM ? acc : acc / dm;
+                mean[cc] = (ACCUM || SEG) ? acc : acc / dm;
             }
         }
+    }
+}
+
+// the segments of a large selection's K4, in segment order, then / m
+__global__ __launch_bounds__(256) void k_mean_comb(const double *__restrict__ part, int S, int64_t d,
+                                                   int m, double *__restrict__ mean) {
+    const double dm = (double)m;
+    for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < d; c += (int64_t)gridDim.x * 256) {
+        double acc = 0.0;
+        for (int y = 0; y < S; ++y) acc += __builtin_nontemporal_load(part + (int64_t)y * d + c);
+        mean[c] = acc / dm;
     }
 }
 
@@ -1750,9 +1777,62 @@ template <bool ACCUM>
 static hipError_t launch_colsum(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel,
                                 int m, double *mean, int num_cu, hipStream_t st);
 
+template <bool SEG>
+static hipError_t launch_mean_seg(const void *X, int dtype, int64_t ld, int64_t d,
+                                  const int64_t *sel, int m, double *out, int num_cu, hipStream_t st);
+
 hipError_t launch_mean(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *sel, int m,
-                       double *mean, int num_cu, hipStream_t st) {
-    return launch_colsum<false>(X, dtype, ld, d, sel, m, mean, num_cu, st);
+                       double *mean, int num_cu, hipStream_t st, double *seg_part) {
+    const int S = mean_segments(m);
+    if (S <= 1 || !seg_part) return launch_colsum<false>(X, dtype, ld, d, sel, m, mean, num_cu, st);
+    // a large selection: the rows in segments of MEAN_SEG_ROWS (grid y), then
+    // the segments in order.  A shard's few columns (config E on 8 GPUs: 32,768
+    // fp32 columns, 8,192 column threads) left most CUs idle with one thread
+    // walking all m rows: 0.25 ms at 1.5 TB/s
+    hipError_t e = launch_mean_seg<true>(X, dtype, ld, d, sel, m, seg_part, num_cu, st);
+    if (e != hipSuccess) return e;
+    int64_t b = (d + 255) / 256;
+    if (b > (int64_t)num_cu * 8) b = (int64_t)num_cu * 8;
+    if (b < 1) b = 1;
+    hipLaunchKernelGGL(k_mean_comb, dim3((unsigned)b), dim3(256), 0, st, seg_part, S, d, m, mean);
+    return hipGetLastError();
+}
+
+template <bool SEG>
+static hipError_t launch_mean_seg(const void *X, int dtype, int64_t ld, int64_t d,
+                                  const int64_t *sel, int m, double *out, int num_cu, hipStream_t st) {
+    const int S = mean_segments(m);
+    const size_t lds = (size_t)MEAN_SEG_ROWS * sizeof(int64_t);
+    const int64_t cap = ((int64_t)num_cu * 16 + S - 1) / S;  // ~16 blocks per CU in all
+    const dim3 block(256);
+    if (dtype != 0 && (ld % 4) == 0 && ((uintptr_t)X % 16) == 0) {
+        int64_t b4 = ((d + 3) / 4 + 255) / 256;
+        b4 = b4 > cap ? cap : b4 < 1 ? 1 : b4;
+        hipLaunchKernelGGL((k_mean_f4<false, true>), dim3((unsigned)b4, (unsigned)S), block, lds, st,
+                           (const float *)X, ld, d, sel, m, out);
+        return hipGetLastError();
+    }
+    int64_t b = ((d + 1) / 2 + 255) / 256;
+    b = b > cap ? cap : b < 1 ? 1 : b;
+    const dim3 grid((unsigned)b, (unsigned)S);
+    const bool vec = dtype == 0 ? ((ld % 2) == 0 && ((uintptr_t)X % 16) == 0)
+                                : ((ld % 2) == 0 && ((uintptr_t)X % 8) == 0);
+    if (dtype == 0) {
+        if (vec)
+            hipLaunchKernelGGL((k_mean<double, true, false, true>), grid, block, lds, st, (const double *)X,
+                               ld, d, sel, m, out);
+        else
+            hipLaunchKernelGGL((k_mean<double, false, false, true>), grid, block, lds, st, (const double *)X,
+                               ld, d, sel, m, out);
+    } else {
+        if (vec)
+            hipLaunchKernelGGL((k_mean<float, true, false, true>), grid, block, lds, st, (const float *)X, ld,
+                               d, sel, m, out);
+        else
+            hipLaunchKernelGGL((k_mean<float, false, false, true>), grid, block, lds, st, (const float *)X, ld,
+                               d, sel, m, out);
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_accumulate(const void *X, int dtype, int64_t ld, int64_t d, const int64_t *idx,
