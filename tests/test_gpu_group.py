@@ -35,7 +35,8 @@ def test_group_of_one_equals_engine_bitwise(engine, oracle, mode):
 
 
 @pytest.mark.parametrize("G", [2, 3, 8])
-@pytest.mark.parametrize("n,d,f", [(100, 7850, 30), (300, 1003, 90), (64, 8 * 8 + 5, 20)])
+@pytest.mark.parametrize("n,d,f", [(100, 7850, 30), (300, 1003, 90), (64, 8 * 8 + 5, 20),
+                                   (1100, 2003, 50)])
 def test_group_host_exchange_matches_oracle(engine, oracle, G, n, d, f):
     """G contexts on device 0: the selection equals the single-context one and
     the oracle's; the mean is column-local, so it is bitwise the single-context
@@ -55,7 +56,9 @@ def test_group_host_exchange_matches_oracle(engine, oracle, G, n, d, f):
     scale = float(np.max(np.mean(np.abs(X[osel]), axis=0)))
     assert float(np.max(np.abs(mean - omean))) <= 1e-9 * scale
     # (64 x 69 at G = 8 leaves ranks 5-7 without columns: that call takes the
-    # one-device path, and must agree all the same)
+    # one-device path, and must agree all the same; 1100 x 2003 with m = 1050
+    # takes K4's row segments, whose order depends on m only, so each device's
+    # few columns add exactly as the single context's)
 
 
 def test_group_small_d_falls_back_to_one_device(engine, oracle):
