@@ -34,6 +34,7 @@ WORKLOADS = {
     "C_1024x131072": dict(n=1024, d=131072, f=307, seed=SEED0 + 3, nbyz=307, dtype="f64"),
     "B_mnist": dict(n=100, d=7850, f=30, seed=SEED0 + 2, nbyz=30, dtype="f64", flags=1),
     "E_4096x262144_fp32": dict(n=4096, d=262144, f=1228, seed=SEED0 + 5, nbyz=1228, dtype="f32"),
+    "A_creditcard": dict(n=10, d=25, f=2, seed=SEED0 + 1, nbyz=2, dtype="f64"),
 }
 DEFAULT_WORKLOAD = "D_512x1M_f153"
 METRIC = "Multi-Krum GB/s (device-resident, n fp64 updates x d) + selected-set parity"
@@ -262,14 +263,15 @@ def graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt):
     return res
 
 
-def small_variant(eng, dev, steps=500, warmup=50):
-    """Config B (mnist softmax: 100 x 7,850 fp64, f = 30), the
-    shape Biscotti's verifiers actually run, device-resident: the one-launch
-    k_small path (bk_set_small_path, default for n <= 128) against the general
-    six-launch chain on the same batch; parity against the B golden."""
+def small_variant(eng, dev, name="B_mnist", steps=500, warmup=50):
+    """Config B (mnist softmax: 100 x 7,850 fp64, f = 30) or A (creditcard:
+    10 x 25, f = 2), the shapes Biscotti's verifiers actually
+    run, device-resident: the one-launch k_small path (bk_set_small_path,
+    default for n <= 128) against the general six-launch chain on the same
+    batch; parity against the config's golden."""
     import torch
     from biscotti_amd import _lib
-    w = WORKLOADS["B_mnist"]
+    w = WORKLOADS[name]
     n, d, f = w["n"], w["d"], w["f"]
     m = n - f
     X = torch.empty((n, d), dtype=torch.float64, device=dev)
@@ -301,7 +303,7 @@ def small_variant(eng, dev, steps=500, warmup=50):
                       "step_roofline": {"t_floor_ms": round(t_floor, 5),
                                         "bound": "hbm" if bytes_alg / PEAK_HBM_GBS > flops / PEAK_TFLOPS["f64"] / 1e3 else "mfma",
                                         "frac": round(t_floor / ms, 4)},
-                      "parity": golden_check("B_mnist", sel.cpu().numpy(), mean.cpu().numpy(), 0, d)}
+                      "parity": golden_check(name, sel.cpu().numpy(), mean.cpu().numpy(), 0, d)}
     eng.set_small_path(True)
     res["ms_per_step"] = res["one_launch"]["ms_per_step"]
     res["value"] = res["one_launch"]["GB_per_s"]
@@ -681,6 +683,7 @@ def main():
 
     if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD:
         out.setdefault("variants", {})["B_mnist"] = small_variant(eng, dev)
+        out["variants"]["A_creditcard"] = small_variant(eng, dev, "A_creditcard")
 
     if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD and not a.no_graph_probe:
         out["hip_graph"] = graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt)

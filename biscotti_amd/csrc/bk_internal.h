@@ -125,6 +125,8 @@ struct SmallPlan {
     int nb16 = 0, nblk = 0, kc = 0, P = 0, ng = 0, Q = 0, nS = 0, C = 0;  // P chunks, ng G items
 };
 SmallPlan small_plan(int n, int64_t d, int num_cu);
+// n <= 16 and d <= 128 (config A): launch_small runs k_tiny, one workgroup
+bool tiny_ok(int n, int64_t d);
 constexpr int SMALL_CTR_WORDS = 71 * 32;  // 71 queue lines of 128 B (bk_small.hip)
 hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,

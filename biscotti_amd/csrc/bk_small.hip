@@ -755,6 +755,122 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     if (a.trace && tid == 0) a.trace[8 * total + 2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
+// k_tiny: the whole call in ONE workgroup for n <= 16, d <= 128 (config A,
+// creditcard: 10 x 25; a real localTest verifier sees n <= 4).  Three
+// hand-offs between CUs (~1 us each) were most of k_small's 15 us there; one
+// workgroup needs none.  Same arithmetic as k_small for a one-chunk batch, so
+// the same bits: the chunk staged alike, the 16 x 16 Gram block by the same
+// MFMA sequence (small_gram_groups), made symmetric from its upper elements,
+// each row's distances in numpy's order, a sort by counting, K2's summation
+// shape (lane t adds rank 1 + t, the wave butterfly, then the four waves'
+// sums in order -- here waves 1-3 hold +0.0), the (score, index) rank, and
+// the mean of the selected rows in ascending order (K4's adds).
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void k_tiny(SmallArgs a) {
+    __shared__ __attribute__((aligned(16))) char tile[16 * SMALL_GR * 16];  // 16 rows x 128 columns
+    __shared__ double gm[16 * 17];          // the Gram block (symmetric)
+    __shared__ uint64_t keys[4][16];        // each wave's row keys
+    __shared__ double srt[4][16];           // each wave's sorted row
+    __shared__ double scs[16];
+    __shared__ uint64_t skey[16];
+    __shared__ double bnd[2];
+    __shared__ uint64_t balw;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int n = a.n, m = n - a.f;
+    const int64_t k = n - a.f - 2 > 0 ? n - a.f - 2 : 0;
+    {
+        SmallStage<T, VEC, 1> st;
+        st.load(a, 0, tid);
+        st.store(tile, 0, SMALL_GR, tid);
+    }
+    __syncthreads();
+    if (wave == 0) {
+        d4 acc[1] = {d4{0.0, 0.0, 0.0, 0.0}};
+        small_gram_groups<1, 0, 0, 1>(acc, tile, lane, 0, SMALL_KC / 8);
+        const int rr = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gm[(g + 4 * r) * 17 + rr] = acc[0][r];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (g + 4 * r > rr) gm[(g + 4 * r) * 17 + rr] = gm[rr * 17 + g + 4 * r];
+    }
+    __syncthreads();
+    // scores: wave w takes rows w, w + 4, ...
+    for (int i = wave; i < n; i += 4) {
+        const double di = gm[i * 17 + i];
+        uint64_t key = ~0ULL;  // padding sorts last
+        if (lane < n) key = dkey((di + gm[lane * 17 + lane]) - 2.0 * gm[i * 17 + lane]);
+        if (lane < 16) keys[wave][lane] = key;
+        __builtin_amdgcn_wave_barrier();
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t o = keys[wave][j];
+            cnt += (o < key) || (o == key && j < lane);
+        }
+        if (lane < 16) srt[wave][cnt] = dkey_inv(key);
+        __builtin_amdgcn_wave_barrier();
+        double acc = 0.0;
+        if (1 + lane <= k) acc += srt[wave][1 + lane];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0) {
+            double sum = 0.0;  // the four waves' sums in order (waves 1-3: +0.0)
+            sum += acc;
+            sum += 0.0;
+            sum += 0.0;
+            sum += 0.0;
+            const double sv = k > 0 ? sum : 0.0;
+            scs[i] = sv;
+            a.scores[i] = sv;
+            a.diag[i] = di;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (tid < 16) skey[tid] = tid < n ? dkey(scs[tid]) : ~0ULL;
+    __syncthreads();
+    if (wave == 0) {
+        bool on = false;
+        if (lane < n) {
+            const uint64_t ki = skey[lane];
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint64_t o = skey[j];
+                cnt += (o < ki) || (o == ki && j < lane);
+            }
+            on = cnt < m;
+            if (cnt == m - 1) bnd[0] = scs[lane];
+            if (cnt == m) bnd[1] = scs[lane];
+        }
+        const uint64_t bal = __ballot(on);
+        if (on && a.sel) a.sel[__popcll(bal & ((1ull << lane) - 1))] = (int64_t)lane;
+        if (lane == 0) balw = bal;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double M = 0.0;
+        for (int j = 0; j < n; ++j) {
+            const double v = gm[j * 17 + j];
+            if (v == v && v < __builtin_inf() && v > M) M = v;
+        }
+        write_margin(a.margin, bnd[0], bnd[1], M, (double)a.d, k, 0x1p-53);
+    }
+    if (a.mean && tid < a.d) {
+        // column tid, the 16 staged rows in ascending order, each row's value
+        // or +0.0 by the selection mask (acc is never -0.0: k_small's M items)
+        const uint64_t sb = balw;
+        double acc = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const double v = reinterpret_cast<const d2v *>(tile + sg_off(r, tid >> 1))[0][tid & 1];
+            acc += ((sb >> r) & 1) ? v : 0.0;
+        }
+        a.mean[tid] = acc / (double)m;
+    }
+}
+
 template <typename T, bool VEC>
 static void launch_small_t(const SmallArgs &a, int NBv, int grid, hipStream_t st) {
     switch (NBv) {
@@ -767,6 +883,14 @@ static void launch_small_t(const SmallArgs &a, int NBv, int grid, hipStream_t st
     case 7: hipLaunchKernelGGL((k_small<T, VEC, 7>), dim3(grid), dim3(256), 0, st, a); break;
     default: hipLaunchKernelGGL((k_small<T, VEC, 8>), dim3(grid), dim3(256), 0, st, a); break;
     }
+}
+
+bool tiny_ok(int n, int64_t d) {
+    static const bool on = [] {
+        const char *e = getenv("BK_TINY");  // 0: k_small for every n <= 128 (A/B)
+        return !(e && atoi(e) == 0);
+    }();
+    return on && n <= 16 && d <= SMALL_KC;
 }
 
 SmallPlan small_plan(int n, int64_t d, int num_cu) {
@@ -813,6 +937,17 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     const int total = SMALL_SPLIT * a.P + a.n + a.C;
     const int grid = total < num_cu ? total : num_cu;
     const bool vec = (ld % 2) == 0 && ((uintptr_t)X % (dtype == 0 ? 16 : 8)) == 0;
+    if (tiny_ok(n, d) && !trace) {  // one workgroup, no hand-offs (k_tiny)
+        if (dtype == 0 && vec)
+            hipLaunchKernelGGL((k_tiny<double, true>), dim3(1), dim3(256), 0, st, a);
+        else if (dtype == 0)
+            hipLaunchKernelGGL((k_tiny<double, false>), dim3(1), dim3(256), 0, st, a);
+        else if (vec)
+            hipLaunchKernelGGL((k_tiny<float, true>), dim3(1), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((k_tiny<float, false>), dim3(1), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (dtype == 0 && vec)
         launch_small_t<double, true>(a, p.nb16, grid, st);
     else if (dtype == 0)

@@ -1,0 +1,84 @@
+"""k_tiny (bk_small.hip): n <= 16, d <= 128 (config A, creditcard 10 x 25;
+a localTest verifier sees n <= 4) runs in ONE workgroup with no hand-offs.
+It is the same arithmetic as k_small for a one-chunk batch, so its selection,
+scores and mean must be BITWISE k_small's.  k_small is reached in a child
+process with BK_TINY=0 (read once per process), on the same synthetic batches.
+The goldens and the chain comparisons of tests/test_gpu_small.py cover k_tiny
+against the reference (their n <= 16 cases now take it)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+# (n, d, f, dtype, ld_pad): creditcard, the localTest n = 4 (k = 0), ragged and fp32 rows
+SHAPES = [(10, 25, 2, "f64", 0), (4, 25, 2, "f64", 0), (16, 128, 5, "f64", 0), (13, 77, 4, "f64", 3),
+          (7, 1, 2, "f64", 0), (16, 100, 6, "f32", 0), (2, 9, 1, "f64", 0)]
+
+CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from biscotti_amd import _lib
+from biscotti_amd.krum import Engine
+out = {}
+e = Engine(0)
+for (n, d, f, dt, pad) in %r:
+    tdt = torch.float32 if dt == "f32" else torch.float64
+    ld = d + pad
+    X = torch.empty((n, ld), dtype=tdt, device="cuda")
+    bdt = _lib.BK_F32 if dt == "f32" else _lib.BK_F64
+    e.synth_fill_ptr(X.data_ptr(), bdt, n, d, ld, 0, d, 1000 + n * 131 + d, f)
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    sc = torch.empty(n, dtype=torch.float64, device="cuda")
+    mn = torch.empty(d, dtype=torch.float64, device="cuda")
+    e.multikrum_device_ptr(X.data_ptr(), bdt, n, d, ld, f, sel.data_ptr(), sc.data_ptr(), mn.data_ptr())
+    e.synchronize()
+    key = "%%d_%%d_%%d_%%s_%%d" %% (n, d, f, dt, pad)
+    out[key + "_sel"] = sel.cpu().numpy()
+    out[key + "_sc"] = sc.cpu().numpy()
+    out[key + "_mn"] = mn.cpu().numpy()
+e.close()
+np.savez(sys.argv[2], **out)
+""" % (SHAPES,)
+
+
+def _run(tmp_path, tiny):
+    env = dict(os.environ)
+    env["BK_TINY"] = "1" if tiny else "0"
+    path = str(tmp_path / ("tiny.npz" if tiny else "small.npz"))
+    r = subprocess.run([sys.executable, "-c", CHILD, REPO, path], env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return np.load(path)
+
+
+def test_tiny_bitwise_equals_k_small(tmp_path):
+    a, b = _run(tmp_path, True), _run(tmp_path, False)
+    assert sorted(a.files) == sorted(b.files)
+    for k in a.files:
+        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+
+
+def test_tiny_is_one_workgroup(engine):
+    """The device entry at config A's shape runs k_tiny: one timed k_small
+    launch (bk_timing id), no K1."""
+    from biscotti_amd import _lib
+    n, d, f = 10, 25, 2
+    X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 20261016, 2)
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    engine.timing_enable(True)
+    engine.multikrum_device_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr(), None, None)
+    engine.synchronize()
+    t = engine.timing_read()
+    engine.timing_enable(False)
+    assert "k_small" in t and "k_gram" not in t, t
+    mg = engine.selection_margin()
+    assert mg["near_tie"] in (False, True)
