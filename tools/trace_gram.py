@@ -98,3 +98,11 @@ for mode in modes:
     print("  WG start: first-round spread %.1f us; last WG end %.1f, first CU idle from %.1f us"
           % (np.sort(starts)[min(ncu, len(starts)) - 1], ends.max(),
              min(np.max(ends[cukey[busy] == k]) for k in np.unique(cukey[busy]))))
+    # per XCD: when its CUs finish, and the clock they held (is the fill loss
+    # a slow XCD, or spread within every XCD?)
+    for x in np.unique(xcc[busy]):
+        sel_x = busy & (xcc == x)
+        cu_end = [np.max((rt1[sel_x & (cukey == k)] - t0) / 100.0) for k in np.unique(cukey[sel_x])]
+        mhz_x = np.median(cyc[sel_x] / np.maximum(dur_us[sel_x], 1e-3))
+        print("  XCD %d: %2d CUs  CU end %.1f..%.1f us (median %.1f)  clock %.0f MHz"
+              % (x, len(cu_end), min(cu_end), max(cu_end), float(np.median(cu_end)), mhz_x))
