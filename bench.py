@@ -66,6 +66,17 @@ def lib_sha16():
     return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
 
 
+def max_over_ranks(v, dev):
+    """The max of a host float over the ranks (on the device with RCCL, on the
+    host with gloo)."""
+    import torch
+    import torch.distributed as tdist
+    on_dev = tdist.get_backend() == "nccl"
+    tt = torch.tensor([v], dtype=torch.float64, device=dev if on_dev else "cpu")
+    tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+    return float(tt.item())
+
+
 def single_call(step, eng, barrier, world, dev, calls=7, idle_s=0.2):
     """What one verifier call sees (krum.go:100-166 runs one Multi-Krum per
     batch): each call starts after >= 150 ms of GPU idle, so the shader clock
@@ -85,9 +96,7 @@ def single_call(step, eng, barrier, world, dev, calls=7, idle_s=0.2):
         torch.cuda.synchronize()
         t = (time.perf_counter() - t0) * 1e3
         if world > 1:
-            tt = torch.tensor([t], dtype=torch.float64, device=dev)
-            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-            t = float(tt.item())
+            t = max_over_ranks(t, dev)
         steps_ms.append(t)
         tr = eng.timing_read()
         tot = tr.get("k_gram", tr.get("k_small", {"total_ms": prev}))["total_ms"]
@@ -99,44 +108,229 @@ def single_call(step, eng, barrier, world, dev, calls=7, idle_s=0.2):
 
 def cpu_baseline(w, target_s=10.0, target_1core_s=6.0):
     """Time the oracle (C/OpenMP restatement of the reference's numpy krum,
-    oracle/krum_oracle.c) on a bounded column sample of the same batch, on all
-    the host threads OpenMP is given and on 1 core."""
+    oracle/krum_oracle.c) on a bounded sample of the same batch, on all the
+    host threads OpenMP is given and on 1 core.  A large
+    batch is sampled by columns (its first ds columns, the same n rows); a batch
+    whose whole Multi-Krum takes well under the target (configs A and B) is
+    run whole, repeatedly, and timed per call."""
     from oracle import oracle as O
     n, d, f = w["n"], w["d"], w["f"]
     dt = np.float32 if w["dtype"] == "f32" else np.float64
     es = 4 if w["dtype"] == "f32" else 8
 
-    def run(ds):
+    def run(ds, reps=1):
         X = O.synth(n, d, w["seed"], w["nbyz"], flags=w.get("flags", 0), dtype=dt, c0=0, dl=ds,
                     d_total=d)
+        O.krum(X, f)  # warm (page-in, thread pool)
         t0 = time.perf_counter()
-        O.krum(X, f)
-        return time.perf_counter() - t0
+        for _ in range(reps):
+            O.krum(X, f)
+        return (time.perf_counter() - t0) / reps
 
     def sized(ds, target):
-        t = run(ds)
+        t, reps = run(ds), 1
         if t < target / 4 and ds < d:
             ds2 = int(min(d, ds * max(1.0, target / max(t, 1e-3))))
             ds2 = max(8, ds2 // 8 * 8)
             if ds2 > ds:
                 ds, t = ds2, run(ds2)
-        return ds, t
+        if ds == d and t < target / 4:  # the whole batch is small: time it per call
+            reps = int(min(100000, max(2, target / 2 / max(t, 1e-6))))
+            t = run(ds, reps)
+        return ds, t, reps
+
+    def what(ds, reps):
+        if reps > 1:
+            return "the whole %dx%d batch, %d calls" % (n, d, reps)
+        return "the first %d of %d columns of the same %dx%d batch" % (ds, d, n, d)
+
+    # first samples of ~2e10 (all cores) / ~1.5e9 (1 core) Gram flops, grown to the target
+    def start(flops):
+        return int(min(d, max(64, flops / (n * n) // 8 * 8)))
 
     cores = O.num_threads()
-    ds, t = sized(min(d, 32768), target_s)
+    ds, t, reps = sized(start(2e10), target_s)
     out = {"value": round(n * ds * es / t / 1e9, 4), "unit": "GB/s", "cores": cores,
-           "cpu_model": cpu_model(), "kind": "port",
+           "cpu_model": cpu_model(), "kind": "port", "ms_per_call": round(t * 1e3, 4),
            "sample": "oracle/krum_oracle.c (OpenMP, %d threads) full Multi-Krum (Gram, sort, "
-                     "select, mean) on the first %d of %d columns of the same %dx%d batch, %.2f s"
-                     % (cores, ds, d, n, d, t)}
+                     "select, mean) on %s, %.3f s per call" % (cores, what(ds, reps), t)}
     O.set_threads(1)
     try:
-        ds1, t1 = sized(min(d, 2048), target_1core_s)
+        ds1, t1, reps1 = sized(start(1.5e9), target_1core_s)
     finally:
         O.set_threads(cores)
     out["value_1core"] = round(n * ds1 * es / t1 / 1e9, 4)
-    out["sample_1core"] = "same, 1 thread, first %d columns, %.2f s" % (ds1, t1)
+    out["ms_per_call_1core"] = round(t1 * 1e3, 4)
+    out["sample_1core"] = "same, 1 thread, %s, %.3f s per call" % (what(ds1, reps1), t1)
     return out
+
+
+F32_MODES = {"exact": 0, "mfma": 1, "certified": 2}  # bk_f32_mode
+
+
+def pmc_traffic(tag):
+    """HBM bytes per launch of the dominant kernel from profiles/pmc_<tag>.json
+    (tools/profile.sh -> tools/pmc_summary.py), used only when that record was
+    taken with this very libbk.so build (sha256 prefix); otherwise null."""
+    path = os.path.join(REPO, "profiles", "pmc_%s.json" % tag)
+    if not os.path.exists(path):
+        return None, "no profiles/pmc_%s.json" % tag
+    try:
+        rec = json.load(open(path))
+    except Exception as e:  # noqa: BLE001
+        return None, "unreadable profiles/pmc_%s.json: %r" % (tag, e)
+    if rec.get("libbk_sha16") != lib_sha16():
+        return None, "stale: profiles/pmc_%s.json is from another libbk.so build" % tag
+    k = rec.get("k_gram") or rec.get("k_small") or {}
+    return k.get("hbm_bytes_per_launch"), "profiles/pmc_%s.json (PMC passes of this libbk.so build)" % tag
+
+
+def workload_tag(name, f32_mode="exact"):
+    return name if f32_mode == "exact" else "%s_%s" % (name, f32_mode)
+
+
+def device_variant(eng, dev, name, f32_mode="exact", steps=20, warmup=5, X=None):
+    """One BASELINE config, device-resident, timed by the driver's own run:
+    W >= 5 warm-up calls, K timed steps bracketed by synchronize, K1 (or
+    k_small) evented live on libbk's stream, the roofline of that kernel
+    (MFMA peak of the arithmetic it runs), its hash-matched PMC traffic, the
+    whole step against its floor, and parity (selection + mean against the
+    reference golden, plus this call's selection margin)."""
+    import torch
+    from biscotti_amd import _lib
+    w = WORKLOADS[name]
+    n, d, f = w["n"], w["d"], w["f"]
+    m = n - f
+    bdt = _lib.BK_F32 if w["dtype"] == "f32" else _lib.BK_F64
+    es = 4 if w["dtype"] == "f32" else 8
+    own = X is None
+    if own:
+        X = torch.empty((n, d), dtype=torch.float32 if es == 4 else torch.float64, device=dev)
+        eng.synth_fill_ptr(X.data_ptr(), bdt, n, d, X.stride(0), 0, d, w["seed"], w["nbyz"],
+                           flags=w.get("flags", 0))
+    sel = torch.empty(m, dtype=torch.int64, device=dev)
+    sc = torch.empty(n, dtype=torch.float64, device=dev)
+    mean = torch.empty(d, dtype=torch.float64, device=dev)
+
+    def step():
+        eng.multikrum_device_ptr(X.data_ptr(), bdt, n, d, X.stride(0), f, sel.data_ptr(),
+                                 sc.data_ptr(), mean.data_ptr())
+
+    eng.set_f32_mode(F32_MODES[f32_mode])
+    try:
+        r0 = eng.certified_reruns()
+        for _ in range(max(5, warmup)):
+            step()
+        torch.cuda.synchronize()
+        k1 = "k_small" if n <= 128 else "k_gram"
+        eng.timing_select([k1])
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        kt = eng.timing_read().get(k1, {"avg_ms": float("nan")})
+        eng.timing_select([])
+        mg = eng.selection_margin()
+        reruns = eng.certified_reruns() - r0
+    finally:
+        eng.set_f32_mode(0)
+    fp32_mma = w["dtype"] == "f32" and f32_mode != "exact" and reruns == 0
+    peak = PEAK_TFLOPS["f32" if fp32_mma else "f64"]
+    flops = n * (n + 1) * d
+    ach = flops / (kt["avg_ms"] * 1e-3) / 1e12
+    traffic, tsrc = pmc_traffic(workload_tag(name, f32_mode))
+    bytes_alg = (n + m) * d * es + 8 * d
+    t_floor = max(flops / (peak * 1e12), bytes_alg / (PEAK_HBM_GBS * 1e9)) * 1e3
+    par = golden_check(name, sel.cpu().numpy(), mean.cpu().numpy(), 0, d) or {}
+    par["margin"] = {"near_tie": mg["near_tie"], "gap": mg["gap"], "err_bound": mg["err_bound"]}
+    out = {"n": n, "d": d, "f": f, "m": m, "dtype": w["dtype"], "f32_mode": f32_mode,
+           "warmup": max(5, warmup), "steps": steps, "ms_per_step": round(ms, 4),
+           "value": round(n * d * es / (ms * 1e-3) / 1e9, 3), "unit": "GB/s",
+           "roofline": {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                        "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": tsrc,
+                        "kernel": k1, "kernel_avg_ms": round(kt["avg_ms"], 4),
+                        "flops_per_launch": flops,
+                        "arithmetic": "fp32 MFMA" if fp32_mma else "fp64 MFMA"},
+           "step_roofline": {"t_floor_ms": round(t_floor, 4), "frac": round(t_floor / ms, 4)},
+           "parity": par}
+    if f32_mode == "certified":
+        out["certified_reruns"] = reruns
+    if traffic:
+        out["roofline"]["traffic_ratio_to_unique_bytes"] = round(traffic / (n * d * es), 3)
+    if own:
+        del X
+    return out
+
+
+def host_entry_variant(eng, dev, name, steps=200, warmup=20, single_calls=7, idle_s=0.2):
+    """What a Biscotti verifier's own call costs (krum.go:100-166: the batch
+    arrives over RPC into host slices): bk_multikrum(BK_HOST_PINNED) from a
+    pinned host batch, H2D + Multi-Krum + D2H of sel and mean, synchronous.
+    Steady state (back-to-back calls) and single calls after idle (the clock
+    ramp), beside the H2D copy alone and the kernel's HIP-event time, with
+    parity against the reference golden."""
+    import ctypes
+    import torch
+    from biscotti_amd import _lib
+    w = WORKLOADS[name]
+    n, d, f = w["n"], w["d"], w["f"]
+    m = n - f
+    Xd = torch.empty((n, d), dtype=torch.float64, device=dev)
+    eng.synth_fill_ptr(Xd.data_ptr(), _lib.BK_F64, n, d, d, 0, d, w["seed"], w["nbyz"],
+                       flags=w.get("flags", 0))
+    Xh = torch.empty((n, d), dtype=torch.float64, pin_memory=True)
+    Xh.copy_(Xd)
+    selh = np.empty(m, dtype=np.int64)
+    meanh = np.empty(d, dtype=np.float64)
+    mo = ctypes.c_int64(0)
+    L = _lib.lib()
+
+    def call():
+        _lib.check(L.bk_multikrum(eng.ctx, ctypes.c_void_p(Xh.data_ptr()), _lib.BK_HOST_PINNED,
+                                  _lib.BK_F64, n, d, d, f, selh.ctypes.data, ctypes.addressof(mo),
+                                  None, meanh.ctypes.data))
+
+    for _ in range(warmup):
+        call()
+    eng.timing_select(["k_small", "k_gram", "h2d"])
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    kt = eng.timing_read()
+    eng.timing_select([])
+    single = []
+    for _ in range(single_calls):
+        torch.cuda.synchronize()
+        time.sleep(idle_s)
+        t0 = time.perf_counter()
+        call()
+        single.append((time.perf_counter() - t0) * 1e3)
+    # the copy alone: the same pinned batch to the device, one H2D per call
+    for _ in range(5):
+        Xd.copy_(Xh, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        Xd.copy_(Xh, non_blocking=True)
+        torch.cuda.synchronize()
+    h2d_ms = (time.perf_counter() - t0) / steps * 1e3
+    kname = "k_small" if "k_small" in kt else "k_gram"
+    par = golden_check(name, selh.copy(), meanh.copy(), 0, d) or {}
+    mg = eng.selection_margin()
+    par["margin"] = {"near_tie": mg["near_tie"], "gap": mg["gap"], "err_bound": mg["err_bound"]}
+    return {"what": "bk_multikrum(BK_HOST_PINNED): H2D of the %dx%d batch + Multi-Krum + D2H of "
+                    "sel and mean, synchronous (the verifier's call, krum.go:100-166)" % (n, d),
+            "n": n, "d": d, "f": f, "steps": steps, "warmup": warmup,
+            "ms_per_call": round(ms, 4), "GB_per_s": round(n * d * 8 / (ms * 1e-3) / 1e9, 3),
+            "single_call_ms_median": round(float(np.median(single)), 4),
+            "single_calls_ms": [round(x, 4) for x in single],
+            "h2d_alone_ms": round(h2d_ms, 4),
+            "overhead_over_h2d_ms": round(ms - h2d_ms, 4),
+            "kernel": kname, "kernel_avg_ms": round(kt.get(kname, {"avg_ms": float("nan")})["avg_ms"], 4),
+            "h2d_evented_ms": round(kt.get("h2d", {"avg_ms": float("nan")})["avg_ms"], 4),
+            "parity": par}
 
 
 def next_rows(eng, X, n, d, sel, m, steps=5):
@@ -395,6 +589,16 @@ def main():
                     help="multi-GPU: all-gather + fixed-order sum instead of all-reduce")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded path + RCCL communicator even at 1 rank")
+    ap.add_argument("--f32-mode", default="exact", choices=sorted(F32_MODES),
+                    help="fp32 workloads (E): exact (fp32 widened onto the fp64 MFMA), mfma "
+                         "(the fp32 MFMA), certified (fp32 MFMA, exact re-run on a near tie)")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="only the workload itself (rocprof PMC passes): no other BASELINE "
+                         "configs, modes or host-entry lines")
+    ap.add_argument("--exchange", default="rccl", choices=("rccl", "host"),
+                    help="N > 1: the packed-Gram exchange inside libbk over RCCL (default), or "
+                         "through torch.distributed gloo on the host (bk_gram_upper_device -> "
+                         "all_reduce -> bk_finish_device; lets N ranks share one GPU in tests)")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="tuning aid on a 1-GPU box: run rank 0's column shard of an N-rank "
                          "job (sharded path, 1-rank RCCL exchange); value is that rank's rate")
@@ -413,12 +617,19 @@ def main():
     from biscotti_amd.dist import bootstrap_rccl, shard_bounds, torch_broadcast_bytes
     from biscotti_amd.krum import Engine
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    host_exch = a.exchange == "host" and world > 1
+    # one rank per GPU; with the host exchange several ranks may share one
+    # (tests run N = 2 on a 1-GPU box)
+    dev_idx = local_rank % max(1, torch.cuda.device_count()) if host_exch else local_rank
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     sharded = world > 1 or a.sharded
     if sharded:
         if not tdist.is_initialized() and "MASTER_ADDR" in os.environ:
-            tdist.init_process_group("nccl", device_id=dev)
+            if host_exch:
+                tdist.init_process_group("gloo")
+            else:
+                tdist.init_process_group("nccl", device_id=dev)
 
     w = WORKLOADS[a.workload]
     n, d, f = w["n"], w["d"], w["f"]
@@ -431,9 +642,10 @@ def main():
     bdt = _lib.BK_F32 if w["dtype"] == "f32" else _lib.BK_F64
     es = 4 if w["dtype"] == "f32" else 8
 
-    eng = Engine(local_rank)
+    eng = Engine(dev_idx)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    if sharded:
+    eng.set_f32_mode(F32_MODES[a.f32_mode])
+    if sharded and not host_exch:
         if tdist.is_initialized():
             bootstrap_rccl(eng, rank, world, torch_broadcast_bytes)
         else:
@@ -447,13 +659,30 @@ def main():
     scores = torch.empty(n, dtype=torch.float64, device=dev)
     mean = torch.empty(max(dl, 1), dtype=torch.float64, device=dev)
 
-    def step():
+    if host_exch:
+        usz = int(_lib.lib().bk_upper_elems(n))
+        Ud = torch.empty(usz, dtype=torch.float64, device=dev)
+        Uh = torch.empty(usz, dtype=torch.float64)
+
+    def step_f(ff, sel_t):
         if not sharded:
-            eng.multikrum_device_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f, sel.data_ptr(),
+            eng.multikrum_device_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), ff, sel_t.data_ptr(),
                                      scores.data_ptr(), mean.data_ptr())
+        elif host_exch:
+            # bk_gram_upper_device -> sum over ranks on the host (gloo) -> bk_finish_device:
+            # the same decomposition as libbk's RCCL exchange (tests/test_gpu_two_process.py)
+            eng.gram_upper_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), Ud.data_ptr())
+            Uh.copy_(Ud)
+            tdist.all_reduce(Uh)
+            Ud.copy_(Uh)
+            eng.finish_ptr(Ud.data_ptr(), X.data_ptr(), bdt, n, dl, X.stride(0), ff,
+                           sel_t.data_ptr(), scores.data_ptr(), mean.data_ptr())
         else:
-            eng.multikrum_sharded_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f, sel.data_ptr(),
+            eng.multikrum_sharded_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), ff, sel_t.data_ptr(),
                                       scores.data_ptr(), mean.data_ptr())
+
+    def step():
+        step_f(f, sel)
 
     def barrier():
         if world > 1:
@@ -494,9 +723,7 @@ def main():
     mg = eng.selection_margin()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = max_over_ranks(elapsed, dev)
     ms_per_step = elapsed / a.steps * 1e3
     value = n * (dl if emu else d) * es / (elapsed / a.steps) / 1e9
 
@@ -506,23 +733,19 @@ def main():
                                                 mean[:dl].cpu().numpy(), c0, dl)
 
     variants = {}
-    if a.workload == "D_512x1M_f153":
+    if a.workload == "D_512x1M_f153" and not a.no_variants:
         # the reference's own clip rule, f = int(0.5 n) (krum.go:110), on the same batch
         f2 = n // 2
         sel2 = torch.empty(n - f2, dtype=torch.int64, device=dev)
 
         def step2():
-            if not sharded:
-                eng.multikrum_device_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f2,
-                                         sel2.data_ptr(), scores.data_ptr(), mean.data_ptr())
-            else:
-                eng.multikrum_sharded_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f2,
-                                          sel2.data_ptr(), scores.data_ptr(), mean.data_ptr())
-        step2()
+            step_f(f2, sel2)
+        for _ in range(max(5, a.warmup)):  # its own warm-up (r2's one call under-warmed it)
+            step2()
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        k2 = max(3, a.steps // 4)
+        k2 = max(10, a.steps // 2)
         t0 = time.perf_counter()
         for _ in range(k2):
             step2()
@@ -531,50 +754,12 @@ def main():
         torch.cuda.synchronize()
         e2 = time.perf_counter() - t0
         if world > 1:
-            tt = torch.tensor([e2], dtype=torch.float64, device=dev)
-            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-            e2 = float(tt.item())
+            e2 = max_over_ranks(e2, dev)
         variants["D_512x1M_f256"] = {
             "f": f2, "m": n - f2, "steps": k2, "ms_per_step": round(e2 / k2 * 1e3, 4),
             "value": round(n * (dl if emu else d) * es / (e2 / k2) / 1e9, 3),
             "parity": EMU_NOTE if emu else golden_check("D_512x1M_f256", sel2.cpu().numpy(),
                                                         mean[:dl].cpu().numpy(), c0, dl)}
-
-    if w["dtype"] == "f32":
-        # config E's "fp32 MFMA path" (bk_set_f32_mode BK_F32_MFMA): the same batch
-        # on v_mfma_f32_16x16x4_f32, fp32 accumulation per K1 segment
-        eng.set_f32_mode(_lib.BK_F32_MFMA)
-        step()
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        k2 = max(3, a.steps // 4)
-        eng.timing_select(["k_gram"])
-        t0 = time.perf_counter()
-        for _ in range(k2):
-            step()
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        e2 = time.perf_counter() - t0
-        kt2 = eng.timing_read()
-        if world > 1:
-            tt = torch.tensor([e2], dtype=torch.float64, device=dev)
-            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-            e2 = float(tt.item())
-        g2 = kt2.get("k_gram", {"avg_ms": float("nan")})
-        variants["f32_mfma"] = {
-            "what": "fp32 rows on the fp32 MFMA (tolerance re-stated, SURVEY §8(d))",
-            "steps": k2, "ms_per_step": round(e2 / k2 * 1e3, 4),
-            "value": round(n * (dl if emu else d) * es / (e2 / k2) / 1e9, 3),
-            "k_gram_ms": round(g2["avg_ms"], 4),
-            "k_gram_tflops": round(n * (n + 1) * dl / (g2["avg_ms"] * 1e-3) / 1e12, 2),
-            "k_gram_frac_of_fp32_peak": round(n * (n + 1) * dl / (g2["avg_ms"] * 1e-3) / 1e12
-                                              / PEAK_TFLOPS["f32"], 4),
-            "parity": EMU_NOTE if emu else golden_check(a.workload, sel.cpu().numpy(),
-                                                        mean[:dl].cpu().numpy(), c0, dl)}
-        eng.set_f32_mode(_lib.BK_F32_EXACT)
-        eng.timing_select([])
 
     # roofline of the dominant kernel (K1, fp64 MFMA): algorithmic flops per
     # launch = n(n+1) * d_local (symmetric Gram incl. diagonal)
@@ -582,22 +767,16 @@ def main():
     g = kt.get(k1name, {"avg_ms": float("nan")})
     flops = n * (n + 1) * dl
     achieved = flops / (g["avg_ms"] * 1e-3) / 1e12
-    peak = PEAK_TFLOPS["f64"]  # fp32 inputs are widened onto the fp64 MFMA path
+    # fp64 rows and exact fp32 rows (widened) run the fp64 MFMA; BK_F32_MFMA /
+    # CERTIFIED the fp32 MFMA
+    fp32_mma = w["dtype"] == "f32" and a.f32_mode != "exact"
+    peak = PEAK_TFLOPS["f32" if fp32_mma else "f64"]
     # traffic: HBM bytes per K1 launch from the rocprofv3 PMC passes
     # (tools/profile.sh -> tools/pmc_summary.py), used only when that record was
     # taken with this very libbk.so build (sha256 prefix); otherwise null
     traffic, traffic_src = None, None
-    pmc_path = os.path.join(REPO, "profiles", "pmc_%s.json" % a.workload)
-    if os.path.exists(pmc_path) and world == 1 and not emu:
-        try:
-            rec = json.load(open(pmc_path))
-            if rec.get("libbk_sha16") == lib_sha16():
-                traffic = rec.get("k_gram", {}).get("hbm_bytes_per_launch")
-                traffic_src = "profiles/pmc_%s.json (PMC passes of this libbk.so build)" % a.workload
-            else:
-                traffic_src = "stale: profiles/pmc_%s.json is from another libbk.so build" % a.workload
-        except Exception:
-            traffic = None
+    if world == 1 and not emu:
+        traffic, traffic_src = pmc_traffic(workload_tag(a.workload, a.f32_mode))
     roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
             "kernel": k1name, "kernel_avg_ms": round(g["avg_ms"], 4),
@@ -629,10 +808,12 @@ def main():
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": w["dtype"],
         "data": "synthetic (repo SplitMix64 spec, generated on device; DESIGN.md)",
         "config": {"workload": a.workload, "n": n, "d": d, "f": f, "m": m,
-                   "parallelism": ("d-shard x%d + RCCL %s" % (world, "all-gather" if a.deterministic else "all-reduce"))
+                   "parallelism": ("d-shard x%d + %s" % (world, "host (gloo) exchange" if host_exch else
+                                                         "RCCL all-gather" if a.deterministic else
+                                                         "RCCL all-reduce"))
                    if sharded and not emu else
                    ("emulated rank 0 of %d (1 GPU)" % emu if emu else "1 GPU"),
-                   "d_local": dl},
+                   "d_local": dl, **({"f32_mode": a.f32_mode} if w["dtype"] == "f32" else {})},
         "roofline": roof,
         "roofline_hbm_k4": k4_roof,
         "step_roofline": step_roof,
@@ -670,9 +851,13 @@ def main():
             tdist.all_gather_object(hs, h)
         ar = kbreak.get("allreduce")
         usz = int(_lib.lib().bk_upper_elems(n))
+        if host_exch:
+            nr = world
         out["rccl"] = {
             "nranks": nr, "rank": rk,
-            "mode": "all-gather + fixed-order sum" if a.deterministic else "all-reduce (sum)",
+            "mode": ("host (gloo all_reduce of the packed partials; test mode, not RCCL)"
+                     if host_exch else
+                     "all-gather + fixed-order sum" if a.deterministic else "all-reduce (sum)"),
             "bytes_per_exchange": usz * 8 * (nr if a.deterministic else 1),
             "exchange_ms_avg": round(ar["avg_ms"], 4) if ar else None,
             "exchanges_this_rank": ex, "bytes_this_rank": by,
@@ -681,9 +866,39 @@ def main():
     if rank == 0 and world == 1 and not emu and not a.no_next_rows and w["dtype"] == "f64":
         out["next_rows"] = next_rows(eng, X, n, d, sel, m)
 
-    if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD:
-        out.setdefault("variants", {})["B_mnist"] = small_variant(eng, dev)
-        out["variants"]["A_creditcard"] = small_variant(eng, dev, "A_creditcard")
+    if rank == 0 and world == 1 and not emu and not a.no_variants:
+        # every other single-GPU BASELINE config in the driver-timed line, each
+        # with its own warm-up, roofline, hash-matched PMC traffic, parity and
+        # CPU baseline at its shape
+        V = out.setdefault("variants", {})
+        cpu = not a.no_cpu_baseline
+        if a.workload == DEFAULT_WORKLOAD:
+            V["C_1024x131072"] = device_variant(eng, dev, "C_1024x131072", steps=20)
+            if cpu:
+                V["C_1024x131072"]["cpu_baseline"] = cpu_baseline(WORKLOADS["C_1024x131072"], 5.0, 3.0)
+        if a.workload == DEFAULT_WORKLOAD or w["dtype"] == "f32":
+            we = WORKLOADS["E_4096x262144_fp32"]
+            XE = X if a.workload == "E_4096x262144_fp32" else None
+            if XE is None:
+                XE = torch.empty((we["n"], we["d"]), dtype=torch.float32, device=dev)
+                eng.synth_fill_ptr(XE.data_ptr(), _lib.BK_F32, we["n"], we["d"], we["d"], 0,
+                                   we["d"], we["seed"], we["nbyz"])
+            for mode in ("exact", "mfma", "certified"):
+                if a.workload == "E_4096x262144_fp32" and mode == a.f32_mode:
+                    continue  # that is the line itself
+                V[workload_tag("E_4096x262144_fp32", mode)] = device_variant(
+                    eng, dev, "E_4096x262144_fp32", mode, steps=10, X=XE)
+            if cpu and "E_4096x262144_fp32" in V:
+                V["E_4096x262144_fp32"]["cpu_baseline"] = cpu_baseline(we, 5.0, 3.0)
+            del XE
+            torch.cuda.empty_cache()
+        if a.workload == DEFAULT_WORKLOAD:
+            for nm in ("B_mnist", "A_creditcard"):
+                V[nm] = small_variant(eng, dev, nm)
+                V[nm]["host_entry"] = host_entry_variant(eng, dev, nm)
+                if cpu:
+                    V[nm]["cpu_baseline"] = cpu_baseline(WORKLOADS[nm], 3.0, 2.0)
+        eng.set_f32_mode(F32_MODES[a.f32_mode])  # the line's own mode for what follows
 
     if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD and not a.no_graph_probe:
         out["hip_graph"] = graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt)

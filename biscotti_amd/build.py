@@ -44,15 +44,35 @@ def needs_build():
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
-def build(force=False, verbose=True, extra=(), out=LIB):
-    """extra/out: debug variants (e.g. -DBK_K1_PROBE into tools/ab/), never the product"""
+def build(force=False, verbose=True, extra=(), out=LIB, jobs=None):
+    """extra/out: debug variants (e.g. -DBK_K1_PROBE into tools/ab/), never the product.
+    Each source compiles to its own object in parallel (every kernel is launched
+    from its own translation unit, so no relocatable device code is needed),
+    then one link."""
     if not force and out == LIB and not needs_build():
         return LIB
-    cmd = [HIPCC] + FLAGS + list(extra) + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out + ".tmp"] + LIBS
+    import concurrent.futures as cf
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="bk_build_")
+    cflags = [f for f in FLAGS if f != "-shared"] + list(extra)
+    objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+
+    def compile_one(i):
+        cmd = [HIPCC] + cflags + ["-c", os.path.join(CSRC, SOURCES[i]), "-o", objs[i]]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    jobs = jobs or min(len(SOURCES), os.cpu_count() or 4, 16)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(compile_one, range(len(SOURCES))))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"] + LIBS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
     return out
 
 

@@ -86,7 +86,14 @@ struct bk_ctx {
     DevBuf small_ctr, small_part;
     DevBuf mean_part;  // K4 of a large selection: per-segment column sums (launch_mean)
     int small_on = 1;
+    uint64_t small_spin_max = SMALL_SPIN_MAX;  // test knob BK_SMALL_SPIN_MAX=<polls>[,<launches>]
+    int64_t small_spin_left = -1;              // ... for this many launches (-1: all)
+    int small_check_lines = 0;                 // debug knob BK_SMALL_CHECK_LINES (bk_create)
     int margin_valid = 0;
+    // a finish ran since its record's error codes were last read (bk_synchronize
+    // reads them: an asynchronous caller learns of an invalid call there)
+    int margin_unchecked = 0;
+    double *hmargin = nullptr;  // pinned: the record, read back with the host outputs
     // BK_F32_CERTIFIED: 1 while the exact re-run of a near-tie call is in progress
     int force_exact = 0;
     int64_t certified_reruns = 0;
@@ -143,6 +150,12 @@ struct bk_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     int deterministic = 0;
+    // the sharded entry's status agreement (sharded_once): the signature of the
+    // last agreed call, and the device word the agreement all-reduces
+    int64_t agreed_n = -1, agreed_f = -1;
+    int agreed_dtype = -1, agreed_det = -1;
+    DevBuf status;
+    int test_fail_exchange = 0;  // test knob BK_TEST_FAIL_BEFORE_EXCHANGE (bk_create)
     int64_t exchanges = 0;        // exchanges of the packed Gram (bk_comm_stats)
     double exchanged_bytes = 0;   // bytes each rank put into them
 };
@@ -181,7 +194,7 @@ void bind_epoch(bk_ctx *c) {
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                       &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
-                      &c->mean_part};
+                      &c->mean_part, &c->status};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -339,8 +352,30 @@ bool f32_mfma_now(const bk_ctx *c, int dtype) {
            (c->f32_mode == BK_F32_MFMA || c->f32_mode == BK_F32_CERTIFIED);
 }
 
+// Everything stage_gram allocates (K1's plan tables and split-K slabs), so a
+// caller can learn of an allocation failure before it launches anything
+int prepare_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld) {
+    if (use_v3(c, dX, dtype, ld)) {
+        Plan3 *p3 = nullptr;
+        CHK(get_plan3(c, n, d, v3_bk(dtype), &p3));
+        return ensure(c->part, (size_t)p3->nvwg * 16 * 4096 * sizeof(double));
+    }
+    const Plan pl = make_plan(n, d, c->num_cu, (size_t)n * d * esize(dtype));
+    return ensure(c->part, (size_t)pl.ntile * pl.S * 4096 * sizeof(double));
+}
+
+// A partial that must still join an exchange after its rank failed: the
+// trailing pair becomes NaN, every sum with it is NaN, and every rank's finish
+// marks the call invalid (MARGIN_POISONED -> BK_ERCCL from bk_synchronize and
+// the margin readers)
+int poison_upper(bk_ctx *c, double *U, int64_t n) {
+    const int64_t T = (n + 63) / 64;
+    HIPCHK(hipMemsetAsync(U + T * (T + 1) / 2 * 4096, 0xFF, 2 * sizeof(double), c->stream));
+    return BK_OK;
+}
+
 // K1 + K1b: packed upper-triangle Gram of this call's columns into U (tiles,
-// then the trailing element = the column count, bk_upper_elems)
+// then the trailing pair {column count, columns on the fp32 MFMA}, bk_upper_elems)
 int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
                double *U, Plan &pl) {
     if (use_v3(c, dX, dtype, ld)) {
@@ -374,7 +409,9 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
                 fclose(fp);
             }
         }
-        CHK(timed(c, BK_K_REDUCE, [&] { return launch_reduce3(part, P3, U, c->stream); }));
+        CHK(timed(c, BK_K_REDUCE, [&] {
+            return launch_reduce3(part, P3, U, c->stream, f32_mfma_now(c, dtype));
+        }));
         return BK_OK;
     }
     pl = make_plan(n, d, c->num_cu, (size_t)n * d * esize(dtype));
@@ -398,14 +435,14 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     }
     CHK(ensure(c->diag, (size_t)n * sizeof(double)));
     CHK(ensure(c->bnd, 2 * sizeof(double)));
-    CHK(ensure(c->margin, 8 * sizeof(double)));
+    CHK(ensure(c->margin, MARGIN_WORDS * sizeof(double)));
     int *mask = (int *)c->mask.p;
     double *diag = (double *)c->diag.p, *bnd = (double *)c->bnd.p;
     const int64_t m = n - f;
     const int64_t k = n - f - 2 > 0 ? n - f - 2 : 0;
-    // unit roundoff of this Gram's accumulation (the margin's bound)
-    const double u_gram = f32_mfma_now(c, dtype) ? 0x1p-24 : 0x1p-53;
-    const double *dcols = U + (size_t)pl.ntile * 4096;  // the packed upper's trailing element
+    // the packed upper's trailing pair {column count, columns on the fp32 MFMA}:
+    // the margin's d and unit roundoff, totals after an exchange
+    const double *dcols = U + (size_t)pl.ntile * 4096;
     const double *Ut = nullptr, *dg = nullptr;
     if (scores_transposed((int)n)) {
         // large n: transposed off-diagonal tiles + contiguous diagonal, so K2
@@ -423,10 +460,11 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     CHK(timed(c, BK_K_RANK,
               [&] { return launch_rank(sc, (int)n, (int)m, mask, bnd, c->stream); }));
     CHK(timed(c, BK_K_COMPACT, [&] {
-        return launch_compact(mask, (int)n, d_sel, diag, bnd, dcols, k, u_gram,
-                              (double *)c->margin.p, c->stream);
+        return launch_compact(mask, (int)n, d_sel, diag, bnd, dcols, k, (double *)c->margin.p,
+                              c->stream);
     }));
     c->margin_valid = 1;
+    c->margin_unchecked = 1;
     if (d_mean && d > 0) {
         double *seg = nullptr;
         if (mean_segments((int)m) > 1) {
@@ -467,7 +505,7 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
     CHK(ensure(c->small_part, (size_t)sp.P * (np16 * np16 + np16) * sizeof(double)));
     CHK(ensure(c->U, (size_t)bk_upper_elems(n) * sizeof(double)));
     CHK(ensure(c->diag, (size_t)n * sizeof(double)));
-    CHK(ensure(c->margin, 8 * sizeof(double)));
+    CHK(ensure(c->margin, MARGIN_WORDS * sizeof(double)));
     double *sc = d_scores;
     if (!sc) {
         CHK(ensure(c->scores, (size_t)n * sizeof(double)));
@@ -483,13 +521,16 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
         HIPCHK(hipMemsetAsync(c->trace.p, 0, twords * sizeof(long long), c->stream));
         trace = (long long *)c->trace.p;
     }
+    const uint64_t spin = c->small_spin_left == 0 ? SMALL_SPIN_MAX : c->small_spin_max;
+    if (c->small_spin_left > 0) --c->small_spin_left;
     CHK(timed(c, BK_K_SMALL, [&] {
         return launch_small(dX, dtype, ld, (int)n, d, (int)f, sp, (double *)c->small_part.p,
                             (double *)c->U.p, sc, (double *)c->diag.p, d_sel, d_mean,
                             (double *)c->margin.p, (unsigned *)c->small_ctr.p, c->num_cu,
-                            c->stream, trace);
+                            c->stream, trace, spin, c->small_check_lines);
     }));
     c->margin_valid = 1;
+    c->margin_unchecked = 1;
     if (tfile) {
         std::vector<long long> h(twords + 6);
         h[0] = items;
@@ -519,6 +560,47 @@ int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
     double *U = (double *)c->U.p;
     CHK(stage_gram(c, dX, dtype, n, d, ld, U, pl));
     return stage_finish(c, U, pl, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
+}
+
+// the error codes a finish can leave in margin[2] (bk_internal.h MARGIN_*)
+int margin_status(const double *mg) {
+    if (mg[2] == MARGIN_HANDOFF_TIMEOUT)
+        return fail(BK_EHIP, "k_small: a hand-off wait timed out; the call's outputs are invalid "
+                             "(sel entries are -1)");
+    if (mg[2] == MARGIN_POISONED)
+        return fail(BK_ERCCL, "a rank failed before the Gram exchange and poisoned its partial; "
+                              "the call's outputs are invalid");
+    if (mg[2] == MARGIN_QUEUE_DIRTY)
+        return fail(BK_EHIP, "k_small: a queue word other than word 0 of its line was written "
+                             "(BK_SMALL_CHECK_LINES)");
+    return BK_OK;
+}
+
+// the last finish's margin record (k_compact: gap, err_bound, near_tie, M,
+// s_lo, s_hi, d, k, then u_G), synchronously
+int read_margin(bk_ctx *c, double (&mg)[MARGIN_WORDS]) {
+    if (!c->margin_valid) return fail(BK_EINVAL, "no Multi-Krum call on this context yet");
+    HIPCHK(hipMemcpyAsync(mg, c->margin.p, sizeof mg, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->margin_unchecked = 0;
+    return margin_status(mg);
+}
+
+// Synchronous host entries: the record comes back with the outputs (queued on
+// the stream before the caller's sync), and its error codes are checked
+int queue_margin_readback(bk_ctx *c) {
+    if (!c->hmargin) {
+        void *p = nullptr;
+        HIPCHK(hipHostMalloc(&p, MARGIN_WORDS * sizeof(double), hipHostMallocPortable));
+        c->hmargin = (double *)p;
+    }
+    HIPCHK(hipMemcpyAsync(c->hmargin, c->margin.p, MARGIN_WORDS * sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+    return BK_OK;
+}
+int check_margin_readback(bk_ctx *c) {  // after the stream has synchronized
+    c->margin_unchecked = 0;
+    return margin_status(c->hmargin);
 }
 
 // Error paths of the host entries: queued H2D copies may still read the
@@ -651,8 +733,79 @@ int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
                                c->stream);
         return e;
     }));
+    CHK(queue_margin_readback(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     drain.armed = false;
+    CHK(check_margin_readback(c));
+    if (m_out) *m_out = m;
+    return BK_OK;
+}
+
+// Host batches of Biscotti's deployed shapes (n <= 128: configs A and B, the
+// mnist and creditcard verifiers) take the one-launch k_small / k_tiny path:
+// ONE H2D of the 16-B-padded batch on the compute stream (<= 32 MiB: no column
+// chunks, no copy stream), the noise added in place by K6 when the verifier
+// noises the batch itself, the kernel, then the outputs and the margin record
+// back, one synchronize.  The device-resident entry's arithmetic, so the same
+// bits.  where == BK_DEVICE skips the copy.
+int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, const double *noise,
+                   int64_t k, int64_t noise_ld, int64_t n, int64_t d, int64_t f, int64_t *sel_idx,
+                   int64_t *m_out, double *scores, double *mean_out, double *noised_out,
+                   int64_t out_ld) {
+    const size_t es = esize(dtype);
+    const int64_t m = n - f;
+    HostDrain drain{c};
+    const void *dX = X;
+    int64_t dld = ld;
+    if (where != BK_DEVICE) {
+        const int64_t epg = (int64_t)(16 / es);
+        dld = (d + epg - 1) / epg * epg;
+        CHK(ensure(c->X, (size_t)n * dld * es));
+        if (k > 0) CHK(ensure(c->noise, (size_t)n * k * d * sizeof(double)));
+        CHK(timed(c, BK_K_H2D, [&] {
+            hipError_t e = hipMemcpy2DAsync(c->X.p, (size_t)dld * es, X, (size_t)ld * es,
+                                            (size_t)d * es, (size_t)n, hipMemcpyHostToDevice,
+                                            c->stream);
+            if (e == hipSuccess && k > 0)
+                e = hipMemcpy2DAsync(c->noise.p, (size_t)d * 8, noise, (size_t)noise_ld * 8,
+                                     (size_t)d * 8, (size_t)(n * k), hipMemcpyHostToDevice,
+                                     c->stream);
+            return e;
+        }));
+        if (k > 0) {
+            double *xd = (double *)c->X.p;
+            CHK(timed(c, BK_K_NOISE, [&] {
+                return launch_noise(xd, dld, n, d, (const double *)c->noise.p, k, d, xd, dld,
+                                    c->num_cu, c->stream);
+            }));
+        }
+        if (noised_out)
+            HIPCHK(hipMemcpy2DAsync(noised_out, (size_t)out_ld * 8, c->X.p, (size_t)dld * 8,
+                                    (size_t)d * 8, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        dX = c->X.p;
+    }
+    CHK(ensure(c->sel, (size_t)n * sizeof(int64_t)));
+    CHK(ensure(c->scores, (size_t)n * sizeof(double)));
+    if (mean_out) CHK(ensure(c->mean, (size_t)d * sizeof(double)));
+    int64_t *dsel = (int64_t *)c->sel.p;
+    double *dsc = (double *)c->scores.p;
+    double *dmean = mean_out ? (double *)c->mean.p : nullptr;
+    CHK(run_small(c, dX, dtype, n, d, dld, f, dsel, dsc, dmean));
+    CHK(timed(c, BK_K_D2H, [&] {
+        hipError_t e = hipMemcpyAsync(sel_idx, dsel, (size_t)m * sizeof(int64_t),
+                                      hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess && scores)
+            e = hipMemcpyAsync(scores, dsc, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream);
+        if (e == hipSuccess && mean_out)
+            e = hipMemcpyAsync(mean_out, dmean, (size_t)d * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream);
+        return e;
+    }));
+    CHK(queue_margin_readback(c));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    drain.armed = false;
+    CHK(check_margin_readback(c));
     if (m_out) *m_out = m;
     return BK_OK;
 }
@@ -668,17 +821,6 @@ struct DeviceGuard {
     }
 };
 
-// the last finish's margin record (k_compact: gap, err_bound, near_tie, M,
-// s_lo, s_hi, d, k), synchronously
-int read_margin(bk_ctx *c, double (&mg)[8]) {
-    if (!c->margin_valid) return fail(BK_EINVAL, "no Multi-Krum call on this context yet");
-    HIPCHK(hipMemcpyAsync(mg, c->margin.p, sizeof mg, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (mg[2] == 2.0)
-        return fail(BK_EHIP, "k_small: a hand-off wait timed out; the last call's outputs are invalid");
-    return BK_OK;
-}
-
 bool certified(const bk_ctx *c, int dtype) {
     return dtype == BK_F32 && c->f32_mode == BK_F32_CERTIFIED;
 }
@@ -692,9 +834,11 @@ bool certified(const bk_ctx *c, int dtype) {
 template <typename F>
 int run_certified(bk_ctx *c, F &&run) {
     CHK(run());
-    double mg[8];
+    double mg[MARGIN_WORDS];
     CHK(read_margin(c, mg));
-    if (mg[2] == 0.0) return BK_OK;
+    // only a near tie of a call whose Gram ran on the fp32 MFMA (u_G > 2^-53)
+    // is re-run: an exact first pass (k_small, n <= 128) would repeat itself
+    if (mg[2] == 0.0 || !(mg[8] > 0x1p-53)) return BK_OK;
     c->force_exact = 1;
     const int st = run();
     c->force_exact = 0;
@@ -726,7 +870,8 @@ const char *bk_kernel_name(int kid) {
 
 int64_t bk_upper_elems(int64_t n) {
     const int64_t T = (n + 63) / 64;
-    return T * (T + 1) / 2 * 4096 + 1;  // + the column count (K3b's margin)
+    // + the trailing pair {column count, columns on the fp32 MFMA} (K3b's margin)
+    return T * (T + 1) / 2 * 4096 + 2;
 }
 
 int bk_create(bk_ctx **out, int device) {
@@ -754,6 +899,16 @@ int bk_create(bk_ctx **out, int device) {
         if (strcmp(v, "v1") == 0) c->gram_variant = 1;
     if (const char *v = getenv("BK_GRAM_MODE")) c->gram_mode = atoi(v);
     if (const char *v = getenv("BK_SMALL")) c->small_on = atoi(v) != 0;
+    // test / debug knobs (tests/test_gpu_errors.py): a hand-off wait that gives
+    // up after this many polls; the queue-line invariant check; a sharded call
+    // that fails before its exchange
+    if (const char *v = getenv("BK_SMALL_SPIN_MAX")) {
+        char *end = nullptr;
+        c->small_spin_max = strtoull(v, &end, 10);
+        if (end && *end == ',') c->small_spin_left = strtoll(end + 1, nullptr, 10);
+    }
+    if (const char *v = getenv("BK_SMALL_CHECK_LINES")) c->small_check_lines = atoi(v) != 0;
+    if (const char *v = getenv("BK_TEST_FAIL_BEFORE_EXCHANGE")) c->test_fail_exchange = atoi(v);
     e = configure_kernels();
     if (e == hipSuccess) e = configure_aggregate_kernels();
     if (e != hipSuccess) {
@@ -775,7 +930,8 @@ void bk_destroy(bk_ctx *c) {
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                           &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
-                          &c->mean_part};
+                          &c->mean_part, &c->status};
+        if (c->hmargin) (void)hipHostFree(c->hmargin);
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
@@ -810,6 +966,10 @@ int bk_synchronize(bk_ctx *c) {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->margin_unchecked) {  // the last finish's error codes (an asynchronous caller's only check)
+        double mg[MARGIN_WORDS];
+        CHK(read_margin(c, mg));
+    }
     return BK_OK;
 }
 
@@ -919,7 +1079,8 @@ int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t
     DeviceGuard dg(c->device);
     if (certified(c, dtype))
         return run_certified(c, [&] { return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean); });
-    if (c->graph_on && c->timing == 0 && !getenv("BK_TRACE_FILE"))
+    // (the debug traces synchronize mid-call, which a stream capture refuses)
+    if (c->graph_on && c->timing == 0 && !getenv("BK_TRACE_FILE") && !getenv("BK_SMALL_TRACE"))
         return run_device_graph(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
     return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
 }
@@ -955,6 +1116,10 @@ int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
         return fail(BK_EINVAL, "bad where=%d", where);
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
+    // n <= 128: one copy and the one-launch path (always exact: no certified re-run)
+    if (small_ok(c, X, dtype, n, d, ld))
+        return run_host_small(c, X, where, ld, dtype, nullptr, 0, 0, n, d, f, sel_idx, m_out,
+                              scores, mean_out, nullptr, 0);
     const size_t es = esize(dtype);
     const void *dX = X;
     int64_t dld = ld;
@@ -974,9 +1139,9 @@ int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
     }
     CHK(run_host_outputs(c, dX, dtype, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out));
     if (certified(c, dtype)) {  // exact re-run of a near tie from the device-resident batch
-        double mg[8];
+        double mg[MARGIN_WORDS];
         CHK(read_margin(c, mg));
-        if (mg[2] != 0.0) {
+        if (mg[2] != 0.0 && mg[8] > 0x1p-53) {
             c->force_exact = 1;
             Plan pl2;
             int st = stage_gram(c, dX, dtype, n, d, dld, U, pl2);
@@ -1012,6 +1177,10 @@ int bk_multikrum_noised(bk_ctx *c, const double *delta, int64_t ld, const double
     if (noised_out && out_ld < d) return fail(BK_EINVAL, "out_ld=%lld < d", (long long)out_ld);
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
+    // n <= 128: one copy of the batch and its noise, K6, the one-launch path
+    if (small_ok(c, delta, BK_F64, n, d, ld))
+        return run_host_small(c, delta, where, ld, BK_F64, k > 0 ? noise : nullptr, k, noise_ld, n,
+                              d, f, sel_idx, m_out, scores, mean_out, noised_out, out_ld);
     const int64_t dld = (d + 1) / 2 * 2;  // 16-B rows: K1 v3 applies
     CHK(ensure(c->X, (size_t)n * dld * sizeof(double)));
     double *dX = (double *)c->X.p;
@@ -1039,7 +1208,17 @@ int bk_gram_upper_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     Plan pl;
-    return stage_gram(c, dX, dtype, n, d, ld, d_upper, pl);
+    int st = c->test_fail_exchange == 2
+                 ? fail(BK_EHIP, "test knob BK_TEST_FAIL_BEFORE_EXCHANGE=2: forced failure")
+                 : stage_gram(c, dX, dtype, n, d, ld, d_upper, pl);
+    if (st != BK_OK) {
+        // a caller that exchanges the partial anyway (so its peers are not left
+        // in the collective) hands every rank an invalid record, not a wrong Gram
+        const std::string msg = g_err;
+        (void)poison_upper(c, d_upper, n);
+        g_err = msg;
+    }
+    return st;
 }
 
 int bk_finish_device(bk_ctx *c, const double *d_upper, const void *dX, int dtype, int64_t n,
@@ -1076,11 +1255,15 @@ int bk_comm_init(bk_ctx *c, int nranks, int rank, const void *id) {
         (void)ncclCommDestroy(c->comm);
         c->comm = nullptr;
     }
+    // the sharded entry's status agreement word, before the communicator (an
+    // allocation failure then fails this rank's init, not a later collective)
+    CHK(ensure(c->status, sizeof(double)));
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof uid);
     RCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
     c->nranks = nranks;
     c->rank = rank;
+    c->agreed_n = c->agreed_f = -1;  // the next sharded call agrees again
     return BK_OK;
 }
 
@@ -1092,24 +1275,74 @@ int bk_comm_set_mode(bk_ctx *c, int deterministic) {
 
 namespace {
 // one pass of the sharded entry: partial Gram of the local columns (zeros for
-// an empty shard), the exchange, then scores/selection and the local mean
+// an empty shard), the exchange, then scores/selection and the local mean.
+//
+// No rank may leave its peers inside the collective.  Everything that can fail
+// before it is an allocation (U, the all-gather buffer, K1's plan and slabs)
+// or a launch.  On the first call of a signature (n, f, dtype, exchange mode),
+// which every rank makes together, the workspace is allocated and the ranks
+// all-reduce (max) a status word before the exchange, so an allocation
+// failure on one rank is an error on every rank (BK_ERCCL on the others).
+// Later calls of the same signature allocate nothing that depends on the rank
+// alone but K1's slabs for a changed d_local; any failure there (or a failed
+// launch) poisons the rank's partial (NaN trailing pair) and the rank still
+// joins the exchange, so every rank's finish marks the call invalid
+// (MARGIN_POISONED) and the failing rank returns its own error.
 int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, int64_t ld,
                  int64_t f, int64_t *d_sel, double *d_scores, double *d_mean) {
     const int64_t usz = bk_upper_elems(n);
-    CHK(ensure(c->U, (size_t)usz * sizeof(double)));
+    const bool exch = c->comm != nullptr;
+    const bool agree = exch && (c->nranks > 1 || c->test_fail_exchange) &&
+                       (n != c->agreed_n || f != c->agreed_f || dtype != c->agreed_dtype ||
+                        c->deterministic != c->agreed_det);
+    int prep = ensure(c->U, (size_t)usz * sizeof(double));
+    if (prep == BK_OK && exch && c->deterministic)
+        prep = ensure(c->Ug, (size_t)usz * c->nranks * sizeof(double));
+    if (prep == BK_OK && dl > 0) prep = prepare_gram(c, dX, dtype, n, dl, ld);
+    if (prep == BK_OK && c->test_fail_exchange == (agree ? 1 : 2))
+        prep = fail(BK_ENOMEM, "test knob BK_TEST_FAIL_BEFORE_EXCHANGE=%d: forced failure",
+                    c->test_fail_exchange);
+    const std::string prep_msg = prep == BK_OK ? std::string() : g_err;
+    if (agree) {
+        double *w = (double *)c->status.p;
+        double mine = prep == BK_OK ? 0.0 : 1.0, any = 0.0;
+        HIPCHK(hipMemcpyAsync(w, &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        RCCLCHK(ncclAllReduce(w, w, 1, ncclDouble, ncclMax, c->comm, c->stream));
+        HIPCHK(hipMemcpyAsync(&any, w, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (prep != BK_OK) {
+            g_err = prep_msg;
+            return prep;
+        }
+        if (any != 0.0)
+            return fail(BK_ERCCL, "a peer rank failed before the Gram exchange (status agreement "
+                                  "of the call's first signature); no exchange was made");
+        c->agreed_n = n;
+        c->agreed_f = f;
+        c->agreed_dtype = dtype;
+        c->agreed_det = c->deterministic;
+    } else if (prep != BK_OK && (!exch || c->U.bytes < (size_t)usz * sizeof(double))) {
+        return prep;  // nothing to join (no communicator), or no partial to poison
+    }
     double *U = (double *)c->U.p;
     Plan pl;
-    if (dl > 0) {
-        CHK(stage_gram(c, dX, dtype, n, dl, ld, U, pl));
-    } else {
-        // an empty column shard (d small against the rank count): a zero
-        // partial (column count 0 too), so this rank still joins the exchange
-        HIPCHK(hipMemsetAsync(U, 0, (size_t)usz * sizeof(double), c->stream));
-        pl.n = (int)n;
-        pl.T = (int)((n + 63) / 64);
-        pl.ntile = pl.T * (pl.T + 1) / 2;
+    pl.n = (int)n;
+    pl.T = (int)((n + 63) / 64);
+    pl.ntile = pl.T * (pl.T + 1) / 2;
+    int st = prep;
+    if (st == BK_OK) {
+        if (dl > 0) {
+            st = stage_gram(c, dX, dtype, n, dl, ld, U, pl);
+        } else {
+            // an empty column shard (d small against the rank count): a zero
+            // partial (column counts 0 too), so this rank still joins the exchange
+            const hipError_t e = hipMemsetAsync(U, 0, (size_t)usz * sizeof(double), c->stream);
+            if (e != hipSuccess) st = fail(BK_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+        }
     }
-    if (c->comm) {  // also at 1 rank, so the exchange is exercised on a 1-GPU box
+    const std::string st_msg = st == BK_OK ? std::string() : g_err;
+    if (st != BK_OK) CHK(poison_upper(c, U, n));
+    if (exch) {  // also at 1 rank, so the exchange is exercised on a 1-GPU box
         hipEvent_t a = nullptr, b = nullptr;
         const bool ton = timing_on(c, BK_K_ALLREDUCE);
         if (ton) {
@@ -1120,7 +1353,6 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
         if (!c->deterministic) {
             RCCLCHK(ncclAllReduce(U, U, (size_t)usz, ncclDouble, ncclSum, c->comm, c->stream));
         } else {
-            CHK(ensure(c->Ug, (size_t)usz * c->nranks * sizeof(double)));
             double *Ug = (double *)c->Ug.p;
             RCCLCHK(ncclAllGather(U, Ug, (size_t)usz, ncclDouble, c->comm, c->stream));
             HIPCHK(launch_sum_ranks(Ug, c->nranks, usz, U, c->stream));
@@ -1131,6 +1363,12 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
         }
         c->exchanged_bytes += (double)usz * sizeof(double) * (c->deterministic ? c->nranks : 1);
         ++c->exchanges;
+    }
+    if (st != BK_OK) {
+        // the rest of the finish still runs, so this rank's record says so too
+        (void)stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, nullptr);
+        g_err = st_msg;
+        return st;
     }
     return stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores,
                         dl > 0 ? d_mean : nullptr);
@@ -1183,7 +1421,7 @@ int bk_selection_margin(bk_ctx *c, double *gap, double *err_bound, int *near_tie
     if (!c) return fail(BK_EINVAL, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
-    double mg[8];
+    double mg[MARGIN_WORDS];
     CHK(read_margin(c, mg));
     if (gap) *gap = mg[0];
     if (err_bound) *err_bound = mg[1];
@@ -1195,13 +1433,17 @@ int bk_selection_margin_record(bk_ctx *c, double *record) {
     if (!c || !record) return fail(BK_EINVAL, "null context / record");
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
-    double mg[8];
+    double mg[MARGIN_WORDS];
     CHK(read_margin(c, mg));
-    memcpy(record, mg, sizeof mg);
+    memcpy(record, mg, 8 * sizeof(double));  // the public record (u_G stays internal)
     return BK_OK;
 }
 
-int64_t bk_certified_reruns(bk_ctx *c) { return c ? c->certified_reruns : 0; }
+int64_t bk_certified_reruns(bk_ctx *c) {
+    if (!c) return 0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return c->certified_reruns;
+}
 
 int bk_set_small_path(bk_ctx *c, int on) {
     if (!c) return fail(BK_EINVAL, "null context");
@@ -1349,6 +1591,12 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
     if (where != BK_HOST && where != BK_HOST_PINNED)
         return fail(BK_EINVAL, "bk_group_multikrum takes host X (where=%d)", where);
     const int G = (int)g->ctx.size();
+    // Biscotti's deployed shapes (n <= 128, small d: configs A and B) are one
+    // launch on one device (k_small); splitting them over devices only adds
+    // copies and an exchange
+    if (small_ok(g->ctx[0], X, dtype, n, d, ld))
+        return bk_multikrum(g->ctx[0], X, where, dtype, n, d, ld, f, sel_idx, m_out, scores,
+                            mean_out);
     for (int r = 0; r < G; ++r) {
         int64_t c0, dl;
         group_shard(d, G, r, &c0, &dl);
@@ -1378,7 +1626,8 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
         CHK(stage_host_pipelined(c, src, ld, dtype, nullptr, 0, 0, n, dl, (char *)g->X[(size_t)r].p,
                                  dl, (double *)g->U[(size_t)r].p, pls[(size_t)r]));
     }
-    // 2. the exchange
+    // 2.-3. the exchange, then per device the finish and the outputs back
+    auto exchange_finish = [&]() -> int {
     if (g->mode == BK_GROUP_ALLREDUCE) {
         RCCLCHK(ncclGroupStart());
         for (int r = 0; r < G; ++r) {
@@ -1475,10 +1724,35 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
                                    hipMemcpyDeviceToHost, c->stream);
             return e;
         }));
+        CHK(queue_margin_readback(c));
     }
     for (int r = 0; r < G; ++r) {
         DeviceGuard dg(g->ctx[(size_t)r]->device);
         HIPCHK(hipStreamSynchronize(g->ctx[(size_t)r]->stream));
+    }
+    for (int r = 0; r < G; ++r) CHK(check_margin_readback(g->ctx[(size_t)r]));
+    return BK_OK;
+    };
+    CHK(exchange_finish());
+    // BK_F32_CERTIFIED (set on the group's contexts): a near tie of a Gram
+    // taken on the fp32 MFMA is re-run exact from the device-resident shards.
+    // Every device holds the same summed record, so device 0's margin decides.
+    bk_ctx *c0x = g->ctx[0];
+    if (certified(c0x, dtype) && c0x->hmargin[2] == 1.0 && c0x->hmargin[8] > 0x1p-53) {
+        for (bk_ctx *c : g->ctx) c->force_exact = 1;
+        int st = BK_OK;
+        for (int r = 0; r < G && st == BK_OK; ++r) {
+            bk_ctx *c = g->ctx[(size_t)r];
+            DeviceGuard dg(c->device);
+            int64_t c0, dl;
+            group_shard(d, G, r, &c0, &dl);
+            st = stage_gram(c, g->X[(size_t)r].p, dtype, n, dl, dl, (double *)g->U[(size_t)r].p,
+                            pls[(size_t)r]);
+        }
+        if (st == BK_OK) st = exchange_finish();
+        for (bk_ctx *c : g->ctx) c->force_exact = 0;
+        CHK(st);
+        ++c0x->certified_reruns;
     }
     drain.armed = false;
     if (m_out) *m_out = m;
@@ -1530,17 +1804,9 @@ int bk_timing_enable(bk_ctx *c, int on) {
     return bk_timing_select(c, on ? ~0u : 0u);
 }
 
-int bk_timing_stride(bk_ctx *c, int every) {
-    if (!c) return fail(BK_EINVAL, "null context");
-    if (every < 1) return fail(BK_EINVAL, "timing stride %d < 1", every);
-    const uint32_t mask = c->timing;
-    c->tstride = every;
-    return bk_timing_select(c, mask);  // clears, keeps the selection
-}
-
-int bk_timing_select(bk_ctx *c, uint32_t mask) {
-    if (!c) return fail(BK_EINVAL, "null context");
-    std::lock_guard<std::mutex> lk(c->mu);
+namespace {
+// drop the accumulated timings and pending events (under c->mu)
+int timing_reset(bk_ctx *c) {
     DeviceGuard dg(c->device);
     HIPCHK(hipStreamSynchronize(c->stream));
     for (auto &ev : c->pending) {
@@ -1553,8 +1819,23 @@ int bk_timing_select(bk_ctx *c, uint32_t mask) {
         c->cnt[i] = 0;
         c->tseq[i] = 0;
     }
-    c->timing = mask;
     return BK_OK;
+}
+}  // namespace
+
+int bk_timing_stride(bk_ctx *c, int every) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    if (every < 1) return fail(BK_EINVAL, "timing stride %d < 1", every);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->tstride = every;
+    return timing_reset(c);  // clears, keeps the selection
+}
+
+int bk_timing_select(bk_ctx *c, uint32_t mask) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->timing = mask;
+    return timing_reset(c);
 }
 
 int bk_timing_read(bk_ctx *c, int kid, double *total_ms, int64_t *count) {

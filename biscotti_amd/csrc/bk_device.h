@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bk_internal.h"
+
 namespace bk {
 
 typedef double d2v __attribute__((ext_vector_type(2)));
@@ -123,7 +125,7 @@ __device__ __forceinline__ double gamma_n(double nn, double u) {
 // The selection margin record (include/bk.h bk_selection_margin; k_compact):
 // from the boundary scores lo (rank m-1) and hi (rank m), M = max finite
 // G_ii, the Gram's column count d and unit roundoff u_gram, and k.
-//   margin[0..7] = {gap, err_bound, near_tie, M, s_lo, s_hi, d, k}
+//   margin[0..7] = {gap, err_bound, near_tie, M, s_lo, s_hi, d, k}, margin[8] = u_G
 __device__ __forceinline__ void write_margin(double *margin, double lo, double hi, double M,
                                              double dg, int64_t k, double u_gram) {
     const double u = 0x1p-53, kk = (double)k;
@@ -143,6 +145,32 @@ __device__ __forceinline__ void write_margin(double *margin, double lo, double h
     margin[5] = hi;
     margin[6] = dg;
     margin[7] = kk;
+    margin[8] = u_gram;  // internal (not in the public 8-double record): the re-run decision
+}
+
+
+// The margin from a packed record's trailing pair {dg, d32}: dg = the Gram's
+// column count, d32 = how many of them were accumulated on the fp32 MFMA
+// (both summed by every exchange).  u_G = 2^-24 as soon as one column was.
+//   dg NaN (a rank poisoned its partial: bk_multikrum_sharded_device) -> the
+//          record is invalid (MARGIN_POISONED)
+//   dg < 1 (a caller's record without a column count, e.g. pack_upper(G, 0))
+//          -> the bound is unknown: err_bound = +inf, near_tie = 1
+__device__ __forceinline__ void write_margin_rec(double *margin, double lo, double hi, double M,
+                                                 double dg, double d32, int64_t k) {
+    if (dg != dg || d32 != d32) {
+        write_margin(margin, lo, hi, M, 0.0, k, 0x1p-53);
+        margin[1] = __builtin_nan("");
+        margin[2] = MARGIN_POISONED;
+        margin[6] = __builtin_nan("");
+        return;
+    }
+    const double u_gram = d32 > 0.0 ? 0x1p-24 : 0x1p-53;
+    write_margin(margin, lo, hi, M, dg, k, u_gram);
+    if (!(dg >= 1.0)) {
+        margin[1] = __builtin_inf();
+        margin[2] = 1.0;
+    }
 }
 
 }  // namespace bk

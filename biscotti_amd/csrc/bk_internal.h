@@ -80,7 +80,9 @@ struct f32m {
     float v;
     __host__ __device__ operator double() const { return v; }
 };
-hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st);
+// f32_mfma: K1 ran on the fp32 MFMA (the record's second trailing element)
+hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st,
+                          bool f32_mfma);
 hipError_t configure_kernels();
 hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan &pl,
                        double *part, hipStream_t st);
@@ -95,10 +97,19 @@ bool scores_transposed(int n);
 hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipStream_t st);
 hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bnd,
                        hipStream_t st);
-// margin: nullable (8 doubles, see k_compact); dcols: the packed upper's trailing element
+// The device margin record: MARGIN_WORDS doubles, the public 8 (bk.h
+// bk_selection_margin_record) then u_G.  margin[2] codes besides 0 / 1 mark
+// the call's outputs invalid (read_margin turns them into errors):
+constexpr int MARGIN_WORDS = 9;
+constexpr double MARGIN_HANDOFF_TIMEOUT = 2.0;  // k_small: a hand-off wait gave up
+constexpr double MARGIN_POISONED = 3.0;         // a shard failed before the exchange
+constexpr double MARGIN_QUEUE_DIRTY = 4.0;      // k_small (BK_SMALL_CHECK_LINES): a queue word
+                                                // other than word 0 of its line was written
+// margin: nullable (MARGIN_WORDS doubles, see k_compact); dcols: the packed upper's two
+// trailing elements {column count, columns accumulated on the fp32 MFMA}
 hipError_t launch_compact(const int *mask, int n, int64_t *sel, const double *diag,
-                          const double *bnd, const double *dcols, int64_t k, double u_gram,
-                          double *margin, hipStream_t st);
+                          const double *bnd, const double *dcols, int64_t k, double *margin,
+                          hipStream_t st);
 // K4 of a large selection (m >= MEAN_SEG_MIN) sums the selected rows in
 // segments of MEAN_SEG_ROWS (seg_part: mean_segments(m) * d doubles), then
 // the segments in order; the order depends on m only
@@ -128,10 +139,12 @@ SmallPlan small_plan(int n, int64_t d, int num_cu);
 // n <= 16 and d <= 128 (config A): launch_small runs k_tiny, one workgroup
 bool tiny_ok(int n, int64_t d);
 constexpr int SMALL_CTR_WORDS = 71 * 32;  // 71 queue lines of 128 B (bk_small.hip)
+constexpr uint64_t SMALL_SPIN_MAX = 1ull << 24;  // polls before a hand-off wait gives up (~1 s)
 hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
-                        hipStream_t st, long long *trace = nullptr);
+                        hipStream_t st, long long *trace = nullptr,
+                        uint64_t spin_max = SMALL_SPIN_MAX, int check_lines = 0);
 hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, int64_t c0,
                         const int64_t *perm, const SynthParams &P, hipStream_t st);
 

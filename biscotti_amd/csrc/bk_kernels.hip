@@ -861,10 +861,16 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
                                                  const int *__restrict__ red,
                                                  const int *__restrict__ wglist,
                                                  double *__restrict__ U, int64_t usz,
-                                                 double dcols) {
-    // the packed upper's trailing element: the Gram's column count (summed
-    // with the tiles by every exchange, so it is the total d; K3b's margin)
-    if (blockIdx.x == 0 && threadIdx.x == 0) U[usz] = dcols;
+                                                 double dcols, double dcols32) {
+    // the packed upper's two trailing elements: the Gram's column count, and
+    // how many of those columns were accumulated at fp32 unit roundoff (the
+    // fp32 MFMA); both are summed with the tiles by every exchange, so after
+    // one they are totals (K3b's margin: the total d, and u_G = 2^-24 as soon
+    // as any shard ran on the fp32 MFMA)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        U[usz] = dcols;
+        U[usz + 1] = dcols32;
+    }
 #ifndef BK_REDUCE_V1
     // 64 elements per block, 2 per lane (16-B loads), 8 slabs in flight per
     // sub-list; the same order of adds as below (bitwise the same U)
@@ -938,7 +944,10 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_reduce(const double *__restrict__ part, int ntile, int S,
                                                 double *__restrict__ U, double dcols) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) U[(int64_t)ntile * 4096] = dcols;  // as k_reduce3
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // as k_reduce3 (v1 never runs the fp32 MFMA)
+        U[(int64_t)ntile * 4096] = dcols;
+        U[(int64_t)ntile * 4096 + 1] = 0.0;
+    }
     const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
     const int e = chunk * 256 + threadIdx.x;
     const double *p = part + (int64_t)u * 4096 + e;
@@ -1428,7 +1437,7 @@ __global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, 
                                                   const double *__restrict__ diag,
                                                   const double *__restrict__ bnd,
                                                   const double *__restrict__ dcols, int64_t k,
-                                                  double u_gram, double *__restrict__ margin) {
+                                                  double *__restrict__ margin) {
     __shared__ int pre[1024];
     __shared__ double mx[16];
     const int tid = threadIdx.x;
@@ -1462,7 +1471,9 @@ __global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, 
     if (tid == 0) {
         double M = 0.0;
         for (int w = 0; w < 16; ++w) M = fmax(M, mx[w]);
-        write_margin(margin, bnd[0], bnd[1], M, *dcols, k, u_gram);
+        // the packed record's trailing pair: the Gram's column count and the
+        // part of it accumulated on the fp32 MFMA (after an exchange: totals)
+        write_margin_rec(margin, bnd[0], bnd[1], M, dcols[0], dcols[1], k);
     }
 }
 
@@ -1766,10 +1777,10 @@ hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bn
 }
 
 hipError_t launch_compact(const int *mask, int n, int64_t *sel, const double *diag,
-                          const double *bnd, const double *dcols, int64_t k, double u_gram,
-                          double *margin, hipStream_t st) {
+                          const double *bnd, const double *dcols, int64_t k, double *margin,
+                          hipStream_t st) {
     hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, st, mask, n, sel, diag, bnd, dcols, k,
-                       u_gram, margin);
+                       margin);
     return hipGetLastError();
 }
 
@@ -1913,14 +1924,16 @@ hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     return hipGetLastError();
 }
 
-hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st) {
+hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st,
+                          bool f32_mfma) {
     const int64_t usz = (int64_t)pl.ntile * 4096;
+    const double d32 = f32_mfma ? (double)pl.d : 0.0;
 #ifndef BK_REDUCE_V1
     hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 64), dim3(256), 0, st, part, pl.d_red,
-                       pl.d_wglist, U, usz, (double)pl.d);
+                       pl.d_wglist, U, usz, (double)pl.d, d32);
 #else
     hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 128), dim3(256), 0, st, part, pl.d_red,
-                       pl.d_wglist, U, usz, (double)pl.d);
+                       pl.d_wglist, U, usz, (double)pl.d, d32);
 #endif
     return hipGetLastError();
 }

@@ -87,6 +87,8 @@ struct SmallArgs {
     double *part, *U, *scores, *diag, *mean, *margin;
     int64_t *sel;
     unsigned *ctr;
+    uint64_t spin_max;  // polls before a wait gives up (~1 s; a test knob lowers it)
+    int check_lines;    // debug: the last workgroup out checks every queue word
     long long *trace;  // debug (BK_SMALL_TRACE): per item {start, waited, end, hw id,
                        // shader clock at start, at end, two in-item stamps}
 };
@@ -141,13 +143,13 @@ __device__ __forceinline__ int xcc_id() {
 
 // wait for a phase's flag (lane 0 polls this XCD's copy), then the workgroup
 // goes on: its loads of the handed-off bytes are sc1 loads, after this barrier
-__device__ __forceinline__ void wg_wait_flag(unsigned *ctr, int flag) {
+__device__ __forceinline__ void wg_wait_flag(unsigned *ctr, int flag, uint64_t spin_max) {
     if (threadIdx.x == 0) {
         const unsigned *p = cline(ctr, flag + xcc_id());
         uint64_t spins = 0;
         while (ctr_load(p) == 0u) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1ull << 24)) {  // ~1 s: never hang the GPU on a broken hand-off
+            if (++spins > spin_max) {  // ~1 s: never hang the GPU on a broken hand-off
                 __hip_atomic_fetch_or(cline(ctr, C_ERR), 1u, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
                 break;
@@ -712,7 +714,7 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
             small_gram<T, VEC, NB>(b, it, wave, olane, tile, &wbuf[wave][0]);
             if (wg_arrive(ctr, C_G, G_GRP, it, NGI, &s_old)) wg_raise(ctr, F_G);
         } else if (it < NGI + a.n) {
-            wg_wait_flag(ctr, F_G);
+            wg_wait_flag(ctr, F_G, a.spin_max);
             if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
             // the S item's chain sums and Gram row live in the (idle) G tile
             d2v *gv2 = reinterpret_cast<d2v *>(tile);
@@ -725,7 +727,7 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
             // row into LDS, so after the scores only LDS work is left
             double *cols = reinterpret_cast<double *>(tile);
             small_mean_stage<T, NB>(b, it - NGI - a.n, ot, cols);
-            wg_wait_flag(ctr, F_S);
+            wg_wait_flag(ctr, F_S, a.spin_max);
             if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
             small_mean<NB>(b, it - NGI - a.n, ot, wave, olane, kbuf, srow, dgl, bnd, balw, rk, cols,
                        a.trace ? a.trace + 8 * it : nullptr);
@@ -741,15 +743,42 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
         }
     }
     // the last workgroup out resets the queue for the next launch (stream
-    // order: the next launch starts after this one has completed) -- every
-    // word of every line
+    // order: the next launch starts after this one has completed)
     if (last_out) {
-        if (tid == 0 && ctr_load(cline(ctr, C_ERR))) {  // a wait gave up: outputs invalid
-            a.margin[0] = __builtin_nan("");
-            a.margin[2] = 2.0;  // read_margin reports BK_EHIP
+        __shared__ unsigned s_err;
+        if (tid == 0) s_err = ctr_load(cline(ctr, C_ERR));
+        __syncthreads();
+        if (s_err) {
+            // a wait gave up: the outputs are invalid.  The margin says so
+            // (read_margin: BK_EHIP, from bk_synchronize, the synchronous
+            // entries and bk_selection_margin*), and so does the data path:
+            // every selected index becomes -1
+            if (tid == 0) {
+                a.margin[0] = __builtin_nan("");
+                a.margin[2] = MARGIN_HANDOFF_TIMEOUT;
+            }
+            if (a.sel && tid < a.n - a.f) a.sel[tid] = -1;
+        }
+        if (a.check_lines) {
+            // debug (BK_SMALL_CHECK_LINES): the reset below clears word 0 of
+            // each line only, because no other word is ever written; check
+            // that invariant over every word of every line, clear any word
+            // that breaks it and report the launch (MARGIN_QUEUE_DIRTY)
+            __shared__ unsigned s_dirty;
+            if (tid == 0) s_dirty = 0;
+            __syncthreads();
+            for (int w = tid; w < C_LINES * 32; w += 256) {
+                if ((w & 31) == 0) continue;
+                if (ctr_load(ctr + w) != 0u) {
+                    __hip_atomic_store(ctr + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_dirty = 1;  // benign race: every writer stores 1
+                }
+            }
+            __syncthreads();
+            if (tid == 0 && s_dirty) a.margin[2] = MARGIN_QUEUE_DIRTY;
         }
         __syncthreads();
-        // only word 0 of each line is ever written
+        // only word 0 of each line is ever written (checked under check_lines)
         if (tid < C_LINES) __hip_atomic_store(ctr + 32 * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (a.trace && tid == 0) a.trace[8 * total + 2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -911,9 +940,11 @@ SmallPlan small_plan(int n, int64_t d, int num_cu) {
 hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
-                        hipStream_t st, long long *trace) {
+                        hipStream_t st, long long *trace, uint64_t spin_max, int check_lines) {
     SmallArgs a;
     a.trace = trace;
+    a.spin_max = spin_max;
+    a.check_lines = check_lines;
     a.X = X;
     a.ld = ld;
     a.d = d;

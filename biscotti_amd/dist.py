@@ -34,16 +34,22 @@ def all_shards(d, world, align=ALIGN):
 
 
 def upper_elems(n):
-    """bk_upper_elems: the 64x64 upper sub-tiles + one trailing element, the
-    Gram's column count (summed by the exchange with the tiles)."""
+    """bk_upper_elems: the 64x64 upper sub-tiles + the trailing pair {column
+    count, columns accumulated on the fp32 MFMA} (summed by the exchange with
+    the tiles; the selection margin's d and unit roundoff)."""
     T = (n + 63) // 64
-    return T * (T + 1) // 2 * 4096 + 1
+    return T * (T + 1) // 2 * 4096 + 2
 
 
-def pack_upper(G, d_cols=0):
+def pack_upper(G, d_cols, d_cols_f32=0):
     """Dense symmetric n x n -> the packed 64x64-sub-tile upper layout libbk
     exchanges (bk_upper_elems(n) doubles, sub-tiles (bi <= bj) row-major, then
-    the column count d_cols the partial was taken over)."""
+    the column count d_cols the partial was taken over and how many of them
+    were accumulated at fp32 unit roundoff).  d_cols is required: the margin's
+    error bound grows with it, and a record with d_cols < 1 makes every
+    selection a near tie (err_bound = +inf)."""
+    if d_cols is None:
+        raise ValueError("pack_upper needs the partial's column count")
     n = G.shape[0]
     T = (n + 63) // 64
     Gp = np.zeros((T * 64, T * 64))
@@ -54,7 +60,7 @@ def pack_upper(G, d_cols=0):
         for bj in range(bi, T):
             out[u] = Gp[bi * 64:(bi + 1) * 64, bj * 64:(bj + 1) * 64]
             u += 1
-    return np.concatenate([out.reshape(-1), [float(d_cols)]])
+    return np.concatenate([out.reshape(-1), [float(d_cols), float(d_cols_f32)]])
 
 
 def unpack_upper(U, n):

@@ -26,7 +26,10 @@
  * concurrently (peer p sends row p with SourceID sid(p) = (p * 7919) % 10007).
  * Output, per iteration:
  *   iter <k> path=<threshold|deadline> n=<n> f=<f> status=<st> near_tie=<0|1>
- *        batch=<sid,...> accepted=<sid,...>
+ *        batch=<sid,...> accepted=<sid,...> k_small=<launches> k_gram=<launches>
+ * (the launches of the one-launch path and of the general chain's K1 this
+ * iteration, from libbk's per-kernel timing: Biscotti's batch shapes must take
+ * k_small straight from the host entry)
  *   peer <k> <sid> <accepted|rejected|stale>
  */
 #define _GNU_SOURCE
@@ -215,6 +218,9 @@ int main(int argc, char **argv)
         fprintf(stderr, "bk_create: %s\n", bk_last_error());
         return 1;
     }
+    /* count which path each Multi-Krum took (HIP events around k_small / K1) */
+    bk_timing_select(g_ctx, (1u << BK_K_SMALL) | (1u << BK_K_GRAM));
+    int64_t prev_small = 0, prev_gram = 0;
     upd_row = (int64_t *)calloc((size_t)rows, sizeof(int64_t));
     upd_sid = (int64_t *)calloc((size_t)rows, sizeof(int64_t));
     accepted = (int64_t *)calloc((size_t)rows, sizeof(int64_t));
@@ -256,7 +262,13 @@ int main(int argc, char **argv)
         printf(" accepted=");
         for (int64_t i = 0; i < n_acc; ++i)
             printf(i ? ",%lld" : "%lld", (long long)upd_sid[accepted[i]]);
-        printf("\n");
+        int64_t ns = 0, ng = 0;
+        double ms = 0.0;
+        bk_timing_read(g_ctx, BK_K_SMALL, &ms, &ns);
+        bk_timing_read(g_ctx, BK_K_GRAM, &ms, &ng);
+        printf(" k_small=%lld k_gram=%lld\n", (long long)(ns - prev_small), (long long)(ng - prev_gram));
+        prev_small = ns;
+        prev_gram = ng;
         for (int64_t p = 0; p < a; ++p)
             printf("peer %d %lld %s\n", it - 5, (long long)peers[p].sid,
                    peers[p].verdict == V_ACCEPTED   ? "accepted"

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 8
+#define BK_ABI_VERSION 9
 
 typedef struct bk_ctx bk_ctx;
 
@@ -74,6 +74,11 @@ void bk_destroy(bk_ctx *ctx);
 /* Run on a caller stream (hipStream_t passed as void*); NULL = own stream. */
 int bk_set_stream(bk_ctx *ctx, void *hip_stream);
 void *bk_get_stream(bk_ctx *ctx);
+/* Waits for the context stream, then reports whether the last Multi-Krum call
+ * on it produced valid outputs: BK_EHIP when k_small's hand-off wait gave up
+ * (its sel entries are then -1), BK_ERCCL when a rank of a sharded call failed
+ * before the exchange (bk_multikrum_sharded_device).  The asynchronous device
+ * entries report these only here and through bk_selection_margin*. */
 int bk_synchronize(bk_ctx *ctx);
 /* C-owned pinned staging for callers that must copy (cgo: Go pointers may not
  * be retained by C, so the shim packs [][]float64 rows here). */
@@ -82,18 +87,24 @@ int bk_stage_free(bk_ctx *ctx, void *pinned);
 
 /* ---- the drop-in: getTopKRUMIndex (krum.go:100-166) + numpy krum ---------
  * X on host (BK_HOST / BK_HOST_PINNED: copied H2D) or device (BK_DEVICE).
- * A host batch crosses PCIe in column chunks (BK_STAGE_CHUNK_BYTES, default
- * 256 MiB) on a copy stream while the previous chunk's partial Gram runs; the
- * chunk partials are summed in chunk order, so results are deterministic.
+ * Biscotti's deployed shapes (n <= 128, d <= 32768: the mnist and creditcard
+ * verifiers, configs A and B) cross PCIe as ONE copy and run the one-launch
+ * path (k_small / k_tiny, see bk_set_small_path).  A larger host batch crosses
+ * PCIe in column chunks (BK_STAGE_CHUNK_BYTES, default 256 MiB) on a copy
+ * stream while the previous chunk's partial Gram runs; the chunk partials are
+ * summed in chunk order, so results are deterministic.
  * Outputs are HOST pointers: sel_idx (m entries), m_out, scores (n, nullable),
- * mean_out (d, nullable).  Synchronous. */
+ * mean_out (d, nullable).  Synchronous; an invalid call (see bk_synchronize)
+ * returns its error here. */
 int bk_multikrum(bk_ctx *ctx, const void *X, int where, int dtype, int64_t n, int64_t d,
                  int64_t ld, int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
                  double *mean_out);
 
 /* Device-resident, asynchronous on the context stream.  All pointers are
  * device pointers; d_sel_idx gets m = n-f ascending indices; d_scores (n) and
- * d_mean (d) are nullable. */
+ * d_mean (d) are nullable.  A failure inside the kernels (k_small's hand-off
+ * timeout) cannot be returned here: bk_synchronize and bk_selection_margin*
+ * report it, and every d_sel_idx entry is -1. */
 int bk_multikrum_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
                         int64_t ld, int64_t f, int64_t *d_sel_idx, double *d_scores,
                         double *d_mean);
@@ -126,7 +137,10 @@ enum bk_f32_mode { BK_F32_EXACT = 0, BK_F32_MFMA = 1, BK_F32_CERTIFIED = 2 };
  * same device-resident batch, whose outputs replace the first run's.  Never
  * silently different from the reference where the exact path is not; the
  * entries become synchronous (the decision reads the margin on the host).
- * bk_group_multikrum runs such contexts as BK_F32_MFMA (check the margin). */
+ * Only a Gram taken on the fp32 MFMA is re-run (the n <= 128 one-launch path
+ * is always exact).  bk_group_multikrum honours it when it is set on the
+ * group's contexts (bk_group_ctx): a near tie re-runs every device's shard
+ * exact from device memory, then exchanges and finishes again. */
 int bk_set_f32_mode(bk_ctx *ctx, int mode);
 /* exact re-runs BK_F32_CERTIFIED has made on this context */
 int64_t bk_certified_reruns(bk_ctx *ctx);
@@ -139,26 +153,36 @@ int64_t bk_certified_reruns(bk_ctx *ctx);
  *               highest selected one (+inf across a finite -> NaN boundary)
  *   err_bound = 2 (e_here + e_ref),  e = 4 k M' (gamma_{d+2}(u_G) + 2u + gamma_k(u))
  *               with M' >= max_i ||x_i||^2 (finite rows), u = 2^-53, u_G the
- *               Gram's unit roundoff here (2^-53, or 2^-24 on the fp32 MFMA),
- *               gamma_j(u) = j u / (1 - j u), d the Gram's total column count
- *               (after a multi-GPU exchange too), k = n - f - 2
- *   near_tie  = !(gap > err_bound)
+ *               Gram's unit roundoff here (2^-53, or 2^-24 once any of its
+ *               columns ran on the fp32 MFMA), gamma_j(u) = j u / (1 - j u),
+ *               d the Gram's total column count (after a multi-GPU exchange
+ *               too; both come from the packed record's trailing pair), k =
+ *               n - f - 2
+ *   near_tie  = !(gap > err_bound); a record without a column count (d < 1,
+ *               e.g. a caller's own packed Gram) has err_bound = +inf and
+ *               near_tie = 1
  * Any fp64 computation of the reference formula in any summation order --
  * numpy's BLAS included -- gives scores within e of the exact ones, so when
  * near_tie = 0 the reference provably selects exactly sel_idx.  near_tie = 1
  * means the boundary is within rounding (or an exact tie, e.g. k = 0 where every
  * score is 0): the lower-index tie rule decided, and numpy's choice may differ.
- * Reads the record of the last call (synchronizes the context stream). */
+ * Reads the record of the last call (synchronizes the context stream); returns
+ * the errors bk_synchronize does when that call's outputs are invalid. */
 int bk_selection_margin(bk_ctx *ctx, double *gap, double *err_bound, int *near_tie);
 /* the whole record: {gap, err_bound, near_tie, M, s_lo, s_hi, d, k} (8 doubles) */
 int bk_selection_margin_record(bk_ctx *ctx, double *record);
 
 /* ---- dimension-sharded stages (one process / device per column shard) ----
  * Packed upper-triangle Gram: bk_upper_elems(n) doubles = the 64x64 upper
- * sub-tiles, then one trailing element holding the column count.  Summing the
- * packed partials of all shards (trailing elements included) gives the Gram of
- * the full batch and its total d, which the selection margin uses. */
+ * sub-tiles, then a trailing pair: the column count, and how many of those
+ * columns were accumulated on the fp32 MFMA.  Summing the packed partials of
+ * all shards (trailing pairs included) gives the Gram of the full batch, its
+ * total d and its unit roundoff, which the selection margin uses. */
 int64_t bk_upper_elems(int64_t n);
+/* On failure d_upper's trailing pair is set to NaN (best effort): a caller
+ * that still joins its exchange, so its peers are not left waiting, hands
+ * every rank a record that bk_finish_device marks invalid (BK_ERCCL from
+ * bk_synchronize / bk_selection_margin*). */
 int bk_gram_upper_device(bk_ctx *ctx, const void *dX, int dtype, int64_t n, int64_t d,
                          int64_t ld, double *d_upper);
 /* Scores + selection from a (summed) packed Gram, then the mean of this
@@ -177,7 +201,14 @@ int bk_comm_set_mode(bk_ctx *ctx, int deterministic);
 /* Partial Gram of the local column shard -> all-reduce -> scores/selection
  * (redundant on every rank) -> mean of the local columns.  Async on stream. */
 /* d_local = 0 is allowed (an empty trailing shard: dX_local, ld and
- * d_mean_local unused); the rank still joins the exchange. */
+ * d_mean_local unused); the rank still joins the exchange.
+ * No rank strands its peers in the collective: the first call of a signature
+ * (n, f, dtype, exchange mode) allocates the workspace and agrees on a status
+ * word (one extra 8-B all-reduce and a host wait), so an allocation failure
+ * is an error on every rank (BK_ERCCL on the peers); a later failure before
+ * the exchange poisons the rank's partial and the rank still joins, so every
+ * rank's bk_synchronize reports BK_ERCCL and the failing rank returns its own
+ * error. */
 int bk_multikrum_sharded_device(bk_ctx *ctx, const void *dX_local, int dtype, int64_t n,
                                 int64_t d_local, int64_t ld, int64_t f, int64_t *d_sel_idx,
                                 double *d_scores, double *d_mean_local);

@@ -37,7 +37,8 @@ def parse(out):
             ints = lambda s: [int(v) for v in s.split(",")] if s else []  # noqa: E731
             iters[int(t[1])] = dict(path=kv["path"], n=int(kv["n"]), f=int(kv["f"]),
                                     status=int(kv["status"]), near_tie=int(kv["near_tie"]),
-                                    batch=ints(kv["batch"]), accepted=ints(kv["accepted"]))
+                                    batch=ints(kv["batch"]), accepted=ints(kv["accepted"]),
+                                    k_small=int(kv["k_small"]), k_gram=int(kv["k_gram"]))
         elif t[0] == "peer":
             peers.setdefault(int(t[1]), {})[int(t[2])] = t[3]
     return iters, peers
@@ -76,8 +77,11 @@ def test_verifier_flow_against_oracle(harness, oracle, tmp_path):
         assert it["f"] == int(0.5 * n)  # krum.go:110
         if n == 1:
             assert it["status"] == -1 and it["accepted"] == []  # reject all
+            assert it["k_small"] == it["k_gram"] == 0
         else:
             assert it["status"] == 0
+            # the host entry took the one-launch path (k_small / k_tiny), never K1
+            assert (it["k_small"], it["k_gram"]) == (1, 0), it
             Xb = X[[sid_row[s] for s in it["batch"]]]
             osel, _, _ = oracle.krum(Xb, it["f"])
             assert it["accepted"] == [it["batch"][i] for i in osel], (k, it)

@@ -148,8 +148,9 @@ def test_certified_host_entry(engine, oracle):
 
 
 def test_margin_of_summed_shards_counts_all_columns(engine):
-    """The packed partials' trailing elements sum to the total d, so the margin
-    after a multi-GPU exchange uses the whole batch's column count."""
+    """The packed partials' trailing pairs sum to the total d (and to 0 fp32-MFMA
+    columns), so the margin after a multi-GPU exchange uses the whole batch's
+    column count."""
     from biscotti_amd.dist import all_shards
     n, d, f = 200, 30011, 60
     X = torch.empty((n, d), dtype=torch.float64, device="cuda")
@@ -160,7 +161,7 @@ def test_margin_of_summed_shards_counts_all_columns(engine):
         U = torch.empty(usz, dtype=torch.float64, device="cuda")
         engine.gram_upper_ptr(X[:, c0:].data_ptr(), _lib.BK_F64, n, dl, X.stride(0), U.data_ptr())
         engine.synchronize()
-        assert float(U[-1]) == dl
+        assert float(U[-2]) == dl and float(U[-1]) == 0.0
         acc += U
     sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
     sc = torch.empty(n, dtype=torch.float64, device="cuda")
@@ -190,3 +191,47 @@ def test_empty_shard_joins_and_finishes(engine):
     assert np.all(sc.cpu().numpy() == 0)
     mg = engine.selection_margin()
     assert mg["near_tie"] and mg["d"] == 0
+    assert mg["err_bound"] == float("inf")  # no column count: the bound is unknown
+
+
+def test_f32_mfma_record_carries_its_roundoff(engine, oracle):
+    """the margin's unit roundoff travels in the packed record, so a
+    finish on another context (a multi-GPU exchange) cannot under-estimate the
+    bound: fp32-MFMA shards mark their columns, and one such shard in the sum
+    makes the whole record u_G = 2^-24."""
+    from biscotti_amd import dist as D
+    from biscotti_amd.krum import Engine
+    n, d, f = 300, 20000, 90
+    X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F32, n, d, d, 0, d, 33, 60)
+    usz = int(_lib.lib().bk_upper_elems(n))
+    shards = D.all_shards(d, 2)
+    other = Engine(0)  # an exact context for shard 1, the finish on a third view
+    try:
+        engine.set_f32_mode(_lib.BK_F32_MFMA)
+        acc = torch.zeros(usz, dtype=torch.float64, device="cuda")
+        for (c0, dl), eng in zip(shards, (engine, other)):
+            U = torch.empty(usz, dtype=torch.float64, device="cuda")
+            eng.gram_upper_ptr(X[:, c0:].data_ptr(), _lib.BK_F32, n, dl, X.stride(0), U.data_ptr())
+            eng.synchronize()
+            assert float(U[-2]) == dl
+            assert float(U[-1]) == (dl if eng is engine else 0.0)
+            acc += U
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        sc = torch.empty(n, dtype=torch.float64, device="cuda")
+        other.finish_ptr(acc.data_ptr(), X.data_ptr(), _lib.BK_F32, n, d, d, f, sel.data_ptr(),
+                         sc.data_ptr(), None)  # an exact context: the record decides
+        other.synchronize()
+        mg = other.selection_margin()
+        sq = oracle.sqnorms(X.cpu().numpy())
+        GU.check_margin(mg, sc.cpu().numpy(), sq, n, f, d, u_gram=2.0 ** -24)
+        # a record without a column count: unknown bound, always a near tie
+        acc[-2] = 0.0
+        acc[-1] = 0.0
+        other.finish_ptr(acc.data_ptr(), X.data_ptr(), _lib.BK_F32, n, d, d, f, sel.data_ptr(),
+                         sc.data_ptr(), None)
+        mg0 = other.selection_margin()
+        assert mg0["near_tie"] and mg0["err_bound"] == float("inf")
+    finally:
+        engine.set_f32_mode(_lib.BK_F32_EXACT)
+        other.close()

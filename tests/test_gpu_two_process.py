@@ -72,7 +72,7 @@ def _worker(rank, world, port, names, q):
             parts = [None] * world
             dist.all_gather_object(parts, (c0, mean[:dl].cpu().numpy()))
             full_mean = np.concatenate([m for _, m in sorted(parts, key=lambda t: t[0])])
-            out[name] = (sel.cpu().numpy(), sc.cpu().numpy(), full_mean, mg, float(Uh[-1]))
+            out[name] = (sel.cpu().numpy(), sc.cpu().numpy(), full_mean, mg, float(Uh[-2]))
             del X, U
             torch.cuda.empty_cache()
         eng.close()
@@ -104,7 +104,7 @@ def test_two_process_sharded_product_path():
             g = GU.load(name)
             sel, sc, mean, mg, dsum = res[r][name]
             p = GU.C.case_params(name)
-            assert dsum == p["d"]  # the trailing elements summed to the total d
+            assert dsum == p["d"]  # the trailing pairs summed to the total d
             assert np.array_equal(sel, g["sel"]), (r, name)
             GU.check_scores(sc, g, rel=1e-9)
             GU.check_mean(mean, g, man[name])
@@ -114,3 +114,71 @@ def test_two_process_sharded_product_path():
     for name in CASES:
         assert np.array_equal(res[0][name][0], res[1][name][0])
         assert np.array_equal(res[0][name][1], res[1][name][1])
+
+
+def _poison_worker(rank, world, port, q):
+    """Rank 1's partial Gram fails (test knob BK_TEST_FAIL_BEFORE_EXCHANGE=2):
+    its bk_gram_upper_device returns the error and poisons the partial, the
+    rank still joins the exchange (so rank 0 is not left waiting), and both
+    ranks' finishes report the call invalid (BK_ERCCL) instead of selecting
+    from a wrong Gram."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), here, os.path.join(here, "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    if rank == 1:
+        os.environ["BK_TEST_FAIL_BEFORE_EXCHANGE"] = "2"
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from biscotti_amd import _lib
+        from biscotti_amd.dist import shard_bounds
+        from biscotti_amd.krum import Engine
+        eng = Engine(0)
+        n, d, f = 300, 20000, 90
+        c0, dl = shard_bounds(d, world, rank)
+        X = torch.empty((n, dl), dtype=torch.float64, device="cuda")
+        eng.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, dl, dl, c0, d, 99, 60)
+        U = torch.empty(int(_lib.lib().bk_upper_elems(n)), dtype=torch.float64, device="cuda")
+        gram_status = 0
+        try:
+            eng.gram_upper_ptr(X.data_ptr(), _lib.BK_F64, n, dl, dl, U.data_ptr())
+        except _lib.BKError as e:
+            gram_status = e.status
+        torch.cuda.synchronize()
+        Uh = U.cpu()
+        dist.all_reduce(Uh)  # joined by both ranks, whatever happened before
+        U.copy_(Uh)
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        eng.finish_ptr(U.data_ptr(), X.data_ptr(), _lib.BK_F64, n, dl, dl, f, sel.data_ptr())
+        fin_status = 0
+        try:
+            eng.synchronize()
+        except _lib.BKError as e:
+            fin_status = e.status
+        eng.close()
+        q.put((rank, (gram_status, fin_status)))
+    except Exception as e:  # surfaced by the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_two_process_failed_rank_poisons_instead_of_stranding():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_poison_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == (0, -4), res  # rank 0: its Gram fine, the summed record invalid
+    assert res[1] == (-3, -4), res  # rank 1: its own error, then the same verdict

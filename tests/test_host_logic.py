@@ -26,8 +26,9 @@ def test_pack_unpack_roundtrip():
     for n in (1, 5, 64, 65, 130):
         A = rng.standard_normal((n, 7))
         G = A @ A.T
-        U = D.pack_upper(G)
+        U = D.pack_upper(G, 7)
         assert U.size == D.upper_elems(n)
+        assert U[-2] == 7.0 and U[-1] == 0.0
         assert np.allclose(D.unpack_upper(U, n), G)
 
 
@@ -37,7 +38,13 @@ def test_packed_partials_sum_to_full_gram(oracle):
     parts = sum(D.pack_upper(oracle.gram(np.ascontiguousarray(X[:, c0:c0 + dl])), dl)
                 for c0, dl in D.all_shards(1000, 3))
     assert np.allclose(parts, full, rtol=1e-12, atol=1e-15)
-    assert parts[-1] == 1000.0  # the trailing element sums to the total column count
+    assert parts[-2] == 1000.0  # the trailing pair sums to the total column count
+    assert parts[-1] == 0.0     # ... none of it on the fp32 MFMA
+
+
+def test_pack_upper_needs_a_column_count():
+    with pytest.raises(ValueError):
+        D.pack_upper(np.eye(3), None)
 
 
 def test_validator_bookkeeping_mirrors_krum_go():
