@@ -100,6 +100,10 @@ struct bk_ctx {
     // RONI: the validation set (bk_roni_set_validation) and per-call scratch
     DevBuf roni_X, roni_y, roni_w, roni_d, roni_cnt, roni_s;
     int64_t roni_nv = 0, roni_dim = 0;
+    // the torch-path (softmax) RONI: its validation set (fp32 samples, int32
+    // labels; bk_roni_softmax_set_validation) and the prepared models
+    DevBuf rmc_X, rmc_y, rmc_ws;
+    int64_t rmc_nv = 0, rmc_din = 0, rmc_C = 0;
     // bk_multikrum_noised: a 2-slot ring of noise chunks, filled on a copy
     // stream while K6 consumes the previous chunk on `stream` (created lazily)
     DevBuf noise;
@@ -194,7 +198,7 @@ void bind_epoch(bk_ctx *c) {
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                       &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
-                      &c->mean_part, &c->status};
+                      &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -930,7 +934,7 @@ void bk_destroy(bk_ctx *c) {
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                           &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
-                          &c->mean_part, &c->status};
+                          &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws};
         if (c->hmargin) (void)hipHostFree(c->hmargin);
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
@@ -2050,6 +2054,104 @@ int bk_roni(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_
         return launch_roni((const double *)c->roni_X.p, c->roni_nv, d, d,
                            (const double *)c->roni_y.p, dw, dd, n, d,
                            (unsigned int *)c->roni_cnt.p, ds, c->stream);
+    }));
+    CHK(timed(c, BK_K_D2H, [&] {
+        return hipMemcpyAsync(scores, ds, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
+                              c->stream);
+    }));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    drain.armed = false;
+    return BK_OK;
+}
+
+// ---- SURVEY.md §8(f) row 4, the torch path: the softmax-model RONI --------
+static int check_roni_softmax(int64_t nv, int64_t din, int64_t ldv, int64_t C, int64_t n,
+                              int64_t ld) {
+    if (nv < 1 || din < 1) return fail(BK_EINVAL, "need nv >= 1 and d_in >= 1");
+    if (ldv < din) return fail(BK_EINVAL, "ldv=%lld < d_in=%lld", (long long)ldv, (long long)din);
+    if (C < 2 || C > 16) return fail(BK_ENOTSUP, "n_classes=%lld outside [2, 16]", (long long)C);
+    if (n < 0) return fail(BK_EINVAL, "n=%lld < 0", (long long)n);
+    if (n > 0 && ld < C * (din + 1))
+        return fail(BK_EINVAL, "ld=%lld < n_classes * (d_in + 1) = %lld", (long long)ld,
+                    (long long)(C * (din + 1)));
+    if (n > 262139) return fail(BK_ENOTSUP, "RONI n=%lld exceeds 262139", (long long)n);
+    if (nv > ((int64_t)1 << 31)) return fail(BK_ENOTSUP, "RONI nv=%lld too large", (long long)nv);
+    return BK_OK;
+}
+
+int bk_roni_softmax_device(bk_ctx *c, const float *d_Xv, int64_t nv, int64_t d_in, int64_t ldv,
+                           const int32_t *d_yv, int64_t n_classes, const double *d_ww,
+                           const double *d_deltas, int64_t n, int64_t ld, double *d_scores) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    CHK(check_roni_softmax(nv, d_in, ldv, n_classes, n, ld));
+    if (!d_Xv || !d_yv || !d_ww || (n > 0 && (!d_deltas || !d_scores)))
+        return fail(BK_EINVAL, "null pointer argument");
+    if (n == 0) return BK_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    CHK(ensure(c->rmc_ws, roni_softmax_ws(n, d_in)));
+    CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
+    return timed(c, BK_K_RONI, [&] {
+        return launch_roni_softmax(d_Xv, nv, d_in, ldv, d_yv, (int)n_classes, d_ww, d_deltas, n,
+                                   ld, (double *)c->rmc_ws.p, (unsigned int *)c->roni_cnt.p,
+                                   d_scores, c->stream);
+    });
+}
+
+int bk_roni_softmax_set_validation(bk_ctx *c, const float *Xv, int64_t nv, int64_t d_in,
+                                   int64_t ldv, const int32_t *yv, int64_t n_classes) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    CHK(check_roni_softmax(nv, d_in, ldv, n_classes, 0, 0));
+    if (!Xv || !yv) return fail(BK_EINVAL, "null Xv / yv");
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    c->rmc_nv = 0;  // invalid until the new set has landed
+    HostDrain drain{c};
+    CHK(ensure(c->rmc_X, (size_t)nv * d_in * sizeof(float)));
+    CHK(ensure(c->rmc_y, (size_t)nv * sizeof(int32_t)));
+    HIPCHK(hipMemcpy2DAsync(c->rmc_X.p, (size_t)d_in * sizeof(float), Xv, (size_t)ldv * sizeof(float),
+                            (size_t)d_in * sizeof(float), (size_t)nv, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->rmc_y.p, yv, (size_t)nv * sizeof(int32_t), hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    drain.armed = false;
+    c->rmc_nv = nv;
+    c->rmc_din = d_in;
+    c->rmc_C = n_classes;
+    return BK_OK;
+}
+
+int bk_roni_softmax(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_t ld,
+                    double *scores) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->rmc_nv < 1) return fail(BK_EINVAL, "no validation set: call bk_roni_softmax_set_validation");
+    const int64_t din = c->rmc_din, C = c->rmc_C, d = C * (din + 1);
+    CHK(check_roni_softmax(c->rmc_nv, din, din, C, n, ld));
+    if (!ww || (n > 0 && (!deltas || !scores))) return fail(BK_EINVAL, "null pointer argument");
+    if (n == 0) return BK_OK;
+    DeviceGuard dg(c->device);
+    HostDrain drain{c};  // error returns: queued H2D copies may still read ww / deltas
+    CHK(ensure(c->roni_w, (size_t)d * sizeof(double)));
+    CHK(ensure(c->roni_d, (size_t)n * d * sizeof(double)));
+    CHK(ensure(c->roni_s, (size_t)n * sizeof(double)));
+    CHK(ensure(c->rmc_ws, roni_softmax_ws(n, din)));
+    CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
+    double *dw = (double *)c->roni_w.p, *dd = (double *)c->roni_d.p, *ds = (double *)c->roni_s.p;
+    CHK(timed(c, BK_K_H2D, [&] {
+        hipError_t e = hipMemcpyAsync(dw, ww, (size_t)d * sizeof(double), hipMemcpyHostToDevice,
+                                      c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpy2DAsync(dd, (size_t)d * sizeof(double), deltas, (size_t)ld * sizeof(double),
+                                 (size_t)d * sizeof(double), (size_t)n, hipMemcpyHostToDevice,
+                                 c->stream);
+        return e;
+    }));
+    CHK(timed(c, BK_K_RONI, [&] {
+        return launch_roni_softmax((const float *)c->rmc_X.p, c->rmc_nv, din, din,
+                                   (const int32_t *)c->rmc_y.p, (int)C, dw, dd, n, d,
+                                   (double *)c->rmc_ws.p, (unsigned int *)c->roni_cnt.p, ds,
+                                   c->stream);
     }));
     CHK(timed(c, BK_K_D2H, [&] {
         return hipMemcpyAsync(scores, ds, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,

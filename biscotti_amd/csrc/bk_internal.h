@@ -131,6 +131,12 @@ hipError_t configure_aggregate_kernels();
 hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, const double *yv,
                        const double *ww, const double *deltas, int64_t n, int64_t ld,
                        unsigned int *cnt, double *scores, hipStream_t st);
+// the torch-path (softmax model) RONI, K8: ws = roni_softmax_ws(n, din) bytes
+size_t roni_softmax_ws(int64_t n, int64_t din);
+hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
+                               const int32_t *yv, int C, const double *ww, const double *deltas,
+                               int64_t n, int64_t ld, double *ws, unsigned int *good,
+                               double *scores, hipStream_t st);
 // bk_small.hip: the whole Multi-Krum of a small batch (n <= 128) in one launch
 struct SmallPlan {
     int nb16 = 0, nblk = 0, kc = 0, P = 0, ng = 0, Q = 0, nS = 0, C = 0;  // P chunks, ng G items

@@ -108,4 +108,158 @@ hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, con
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// K8: the torch-path RONI (the mnist / lfw softmax verifiers) --
+// client_obj.roni(ww, delta), ML/Pytorch/client_obj.py:100-112: the flat
+// weights [W (C x D_in, row-major), b (C)] rounded to fp32 after the fp64
+// add (SoftmaxModel.reshape -> torch.FloatTensor, softmax_model.py:19-24), the
+// training error 1 - accuracy of argmax(x W^T + b) (client.py:131-139), and
+// score = err(ww + delta) - err(ww).  d = 7,850 for mnist: the model no longer
+// fits K7's LDS layout, and the error is a 10-way argmax, not a sign.
+//
+//   K8a k_roni_mc_prep   Wm[j][k][c] = fp32(ww + delta_j) widened to fp64,
+//                        classes padded to 16 (one 128-B row per feature, so
+//                        a wave's model row is read with wave-uniform scalar
+//                        loads), bm[j][c] the biases
+//   K8b k_roni_mc_count  grid (64-sample chunks, groups of 4 models): wave w
+//                        runs model 4 y + w, lane l sample 64 x + l.  The
+//                        chunk's samples are staged 64 features at a time in
+//                        LDS, transposed ([k][sample]: a lane's reads are
+//                        consecutive words); each lane runs C fp64 FMA chains
+//                        over k ascending (every fp32 x fp32 product is exact
+//                        in fp64), adds the bias, rounds the logits to fp32,
+//                        takes np.argmax (first maximum; a NaN is the maximum)
+//                        and the wave counts correct predictions (ballot).
+//   K8c k_roni_mc_score  score[i] = (1 - good[i+1]/nv) - (1 - good[0]/nv)
+//
+// Bound: fp64 VALU (nv x (n+1) x C x D_in FMAs); the samples are re-read
+// once per 4 models (L2), the models once per 64 samples (scalar cache).
+constexpr int RMC_S = 64, RMC_M = 4, RMC_KC = 64, RMC_CP = 16;
+
+__global__ __launch_bounds__(256) void k_roni_mc_prep(const double *__restrict__ ww,
+                                                      const double *__restrict__ deltas, int64_t ld,
+                                                      int64_t din, int C, double *__restrict__ Wm,
+                                                      double *__restrict__ bm) {
+    const int64_t j = blockIdx.y;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // k * 16 + c
+    const int64_t k = e >> 4;
+    const int c = (int)(e & 15);
+    if (k < din) {
+        double v = 0.0;  // padding classes: zero weights, never compared
+        if (c < C) {
+            const int64_t idx = (int64_t)c * din + k;
+            v = (double)(float)(j == 0 ? ww[idx] : ww[idx] + deltas[(j - 1) * ld + idx]);
+        }
+        Wm[(j * din + k) * RMC_CP + c] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < RMC_CP) {
+        const int cc = (int)threadIdx.x;
+        double v = 0.0;
+        if (cc < C) {
+            const int64_t idx = (int64_t)C * din + cc;
+            v = (double)(float)(j == 0 ? ww[idx] : ww[idx] + deltas[(j - 1) * ld + idx]);
+        }
+        bm[j * RMC_CP + cc] = v;
+    }
+}
+
+// NC: classes computed (compile time); C: classes compared (C <= NC)
+template <int NC>
+__global__ __launch_bounds__(256) void k_roni_mc_count(const float *__restrict__ Xv, int64_t nv,
+                                                       int64_t din, int64_t ldv,
+                                                       const int32_t *__restrict__ yv, int C,
+                                                       const double *__restrict__ Wm,
+                                                       const double *__restrict__ bm, int64_t nmod,
+                                                       unsigned int *__restrict__ good) {
+    __shared__ float xs[RMC_KC][RMC_S + 1];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t j = (int64_t)blockIdx.y * RMC_M + wave;
+    const int64_t jj = j < nmod ? j : nmod - 1;  // an idle wave reads a real model, never counts
+    const int64_t s0 = (int64_t)blockIdx.x * RMC_S;
+    const double *wj = Wm + jj * din * RMC_CP;
+    double acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+    // staging: thread t moves features (t & 3) * 16 .. + 15 of sample t >> 2
+    const int ts = tid >> 2, tk = (tid & 3) * 16;
+    const int64_t srow = s0 + ts < nv ? s0 + ts : nv - 1;
+    const float *xrow = Xv + srow * ldv;
+    for (int64_t k0 = 0; k0 < din; k0 += RMC_KC) {
+        __syncthreads();  // the previous chunk has been consumed
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int64_t k = k0 + tk + u;
+            xs[tk + u][ts] = k < din ? xrow[k] : 0.0f;
+        }
+        __syncthreads();
+        const int kn = (int)(din - k0 < RMC_KC ? din - k0 : RMC_KC);
+        const double *wk = wj + k0 * RMC_CP;
+        for (int kk = 0; kk < kn; ++kk) {
+            const double x = (double)xs[kk][lane];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c] = __builtin_fma(x, wk[kk * RMC_CP + c], acc[c]);
+        }
+    }
+    // logits in fp32, np.argmax: the first maximum, a NaN wins at its first place
+    int best = 0;
+    float bl = 0.0f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (c >= C) break;
+        const float lg = (float)(acc[c] + bm[jj * RMC_CP + c]);
+        if (c == 0) {
+            bl = lg;
+        } else if (!(bl != bl) && (lg != lg || lg > bl)) {
+            best = c;
+            bl = lg;
+        }
+    }
+    const int64_t s = s0 + lane;
+    const bool ok = s < nv && best == yv[s < nv ? s : nv - 1];
+    const unsigned int cnt = (unsigned int)__popcll(__ballot(ok));
+    if (lane == 0 && j < nmod && cnt) atomicAdd(&good[j], cnt);
+}
+
+__global__ void k_roni_mc_score(const unsigned int *__restrict__ good, int64_t n, int64_t nv,
+                                double *__restrict__ scores) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double dn = (double)nv;
+    const double orig = 1.0 - (double)good[0] / dn;  // 1 - accuracy_score
+    const double after = 1.0 - (double)good[i + 1] / dn;
+    scores[i] = after - orig;
+}
+
+size_t roni_softmax_ws(int64_t n, int64_t din) {
+    return (size_t)(n + 1) * ((size_t)din * RMC_CP + RMC_CP) * sizeof(double);
+}
+
+hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
+                               const int32_t *yv, int C, const double *ww, const double *deltas,
+                               int64_t n, int64_t ld, double *ws, unsigned int *good,
+                               double *scores, hipStream_t st) {
+    const int64_t nmod = n + 1;
+    double *Wm = ws, *bm = ws + (size_t)nmod * din * RMC_CP;
+    hipError_t e = hipMemsetAsync(good, 0, (size_t)nmod * sizeof(unsigned int), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_roni_mc_prep, dim3((unsigned)((din * RMC_CP + 255) / 256), (unsigned)nmod),
+                       dim3(256), 0, st, ww, deltas, ld, din, C, Wm, bm);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const dim3 grid((unsigned)((nv + RMC_S - 1) / RMC_S), (unsigned)((nmod + RMC_M - 1) / RMC_M));
+    if (C == 2)
+        hipLaunchKernelGGL(k_roni_mc_count<2>, grid, dim3(256), 0, st, Xv, nv, din, ldv, yv, C, Wm, bm, nmod, good);
+    else if (C == 10)
+        hipLaunchKernelGGL(k_roni_mc_count<10>, grid, dim3(256), 0, st, Xv, nv, din, ldv, yv, C, Wm, bm, nmod, good);
+    else if (C == 12)
+        hipLaunchKernelGGL(k_roni_mc_count<12>, grid, dim3(256), 0, st, Xv, nv, din, ldv, yv, C, Wm, bm, nmod, good);
+    else
+        hipLaunchKernelGGL(k_roni_mc_count<RMC_CP>, grid, dim3(256), 0, st, Xv, nv, din, ldv, yv, C, Wm, bm, nmod, good);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_roni_mc_score, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, good,
+                       n, nv, scores);
+    return hipGetLastError();
+}
+
 }  // namespace bk

@@ -19,7 +19,7 @@ import numpy as np
 from ._lib import check, lib
 from .krum import Engine, Update, default_engine
 
-__all__ = ["RONI_THRESHOLD", "RONIValidator", "set_validation", "roni"]
+__all__ = ["RONI_THRESHOLD", "RONIValidator", "SoftmaxRONIValidator", "set_validation", "roni"]
 
 RONI_THRESHOLD = 0.02  # main.go:213
 
@@ -64,6 +64,39 @@ class RONIValidator:
         if self.priv_prob > 0:
             return np.ones(len(updates), dtype=bool)
         return ~(sc > RONI_THRESHOLD)
+
+
+class SoftmaxRONIValidator(RONIValidator):
+    """The torch-path verifier (ML/Pytorch/client_obj.py:100-112: the mnist /
+    lfw softmax models): err = 1 - accuracy of argmax(x W^T + b) over the
+    validation samples (client.py:131-139), the flat weights [W (C x d_in),
+    b (C)] rounded to fp32 as SoftmaxModel.reshape does.  One validation set
+    resident on one GPU (bk_roni_softmax_set_validation)."""
+
+    def __init__(self, Xvalid, yvalid, n_classes, engine: Optional[Engine] = None,
+                 priv_prob: float = 0.0):
+        self._engine = engine if engine is not None else default_engine(0)
+        X = np.ascontiguousarray(Xvalid, dtype=np.float32)
+        y = np.ascontiguousarray(yvalid, dtype=np.int32)
+        if X.ndim != 2 or y.shape != (X.shape[0],):
+            raise ValueError("Xvalid must be (nv, d_in) and yvalid (nv,)")
+        self.nv, self.d_in = X.shape
+        self.n_classes = int(n_classes)
+        self.d = self.n_classes * (self.d_in + 1)
+        self.priv_prob = priv_prob
+        check(lib().bk_roni_softmax_set_validation(self._engine.ctx, X.ctypes.data, self.nv,
+                                                   self.d_in, self.d_in, y.ctypes.data,
+                                                   self.n_classes))
+
+    def scores(self, ww, deltas) -> np.ndarray:
+        ww = np.ascontiguousarray(ww, dtype=np.float64)
+        D = np.ascontiguousarray(np.atleast_2d(deltas), dtype=np.float64)
+        if ww.shape != (self.d,) or D.shape[1] != self.d:
+            raise ValueError("ww must be (d,) and deltas (n, d) with d = %d" % self.d)
+        out = np.empty(D.shape[0], dtype=np.float64)
+        check(lib().bk_roni_softmax(self._engine.ctx, ww.ctypes.data, D.ctypes.data, D.shape[0],
+                                    self.d, out.ctypes.data))
+        return out
 
 
 _validator: Optional[RONIValidator] = None

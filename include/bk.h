@@ -334,6 +334,29 @@ int bk_roni_set_validation(bk_ctx *ctx, const double *Xv, int64_t nv, int64_t d,
 int bk_roni(bk_ctx *ctx, const double *ww, const double *deltas, int64_t n, int64_t d, int64_t ld,
             double *scores);
 
+/* The torch-path RONI verifier (the mnist / lfw softmax models) --
+ * client_obj.roni(ww, delta), ML/Pytorch/client_obj.py:100-112, batched over
+ * n updates:
+ *     score[i] = err(ww + delta_i) - err(ww),
+ *     err(w)   = 1 - mean(argmax_c(x W^T + b) == y)   over the validation set
+ * with w = [W (n_classes x d_in, row-major), b (n_classes)] (SoftmaxModel,
+ * ML/Pytorch/softmax_model.py:19-24; d = n_classes * (d_in + 1): mnist
+ * 10 x 785 = 7,850) rounded to fp32 after the fp64 add (torch.FloatTensor),
+ * each logit the fp64 sum over k ascending of the exact fp32 products plus the
+ * bias, rounded once to fp32; argmax as numpy's (first maximum, NaN wins).
+ * Xv is nv x d_in fp32 (row stride ldv), yv the nv labels (int32).
+ * 2 <= n_classes <= 16. */
+int bk_roni_softmax_device(bk_ctx *ctx, const float *d_Xv, int64_t nv, int64_t d_in, int64_t ldv,
+                           const int32_t *d_yv, int64_t n_classes, const double *d_ww,
+                           const double *d_deltas, int64_t n, int64_t ld, double *d_scores);
+/* The Go verifier's shape (verifyUpdate, honest.go:598-629, bound to the
+ * torch module's roni): the validation set once per context, then host
+ * updates scored against the chain's latest model; synchronous. */
+int bk_roni_softmax_set_validation(bk_ctx *ctx, const float *Xv, int64_t nv, int64_t d_in,
+                                   int64_t ldv, const int32_t *yv, int64_t n_classes);
+int bk_roni_softmax(bk_ctx *ctx, const double *ww, const double *deltas, int64_t n, int64_t ld,
+                    double *scores);
+
 /* ---- measurement: per-kernel HIP-event timing on the context stream ------- */
 enum bk_kernel_id {
     BK_K_GRAM = 0,     /* K1  fp64-MFMA split-K upper-triangle Gram partials */

@@ -57,6 +57,9 @@ def lib():
         L.oracle_noise.restype = None
         L.oracle_roni.argtypes = [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _vp]
         L.oracle_roni.restype = ctypes.c_int
+        L.oracle_roni_softmax.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64,
+                                           _i64, _vp]
+        L.oracle_roni_softmax.restype = ctypes.c_int
         L.oracle_go_f64_to_i64.argtypes = [ctypes.c_double]
         L.oracle_go_f64_to_i64.restype = _i64
         L.oracle_num_threads.restype = ctypes.c_int
@@ -219,4 +222,20 @@ def roni(Xv, yv, ww, deltas):
     out = np.empty(D.shape[0], dtype=np.float64)
     assert lib().oracle_roni(_ptr(Xv), nv, d, d, _ptr(yv), _ptr(ww), _ptr(D), D.shape[0], d,
                              _ptr(out)) == 0
+    return out
+
+
+def roni_softmax(Xv, yv, n_classes, ww, deltas):
+    """ML/Pytorch/client_obj.py:100-112 (softmax model, getTrainErr) for each
+    row of deltas: scores (n,).  Xv (nv, d_in) float32, yv (nv,) int labels, ww
+    and deltas fp64 of length n_classes * (d_in + 1) ([W row-major, b])."""
+    Xv = np.ascontiguousarray(Xv, dtype=np.float32)
+    yv = np.ascontiguousarray(yv, dtype=np.int32)
+    ww = np.ascontiguousarray(ww, dtype=np.float64)
+    D = np.ascontiguousarray(np.atleast_2d(deltas), dtype=np.float64)
+    nv, din = Xv.shape
+    assert ww.shape == (n_classes * (din + 1),) and D.shape[1] == ww.shape[0]
+    out = np.empty(D.shape[0], dtype=np.float64)
+    assert lib().oracle_roni_softmax(_ptr(Xv), nv, din, din, _ptr(yv), int(n_classes), _ptr(ww),
+                                     _ptr(D), D.shape[0], D.shape[1], _ptr(out)) == 0
     return out
