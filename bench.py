@@ -671,10 +671,14 @@ def main():
         elif host_exch:
             # bk_gram_upper_device -> sum over ranks on the host (gloo) -> bk_finish_device:
             # the same decomposition as libbk's RCCL exchange (tests/test_gpu_two_process.py)
+            # (libbk runs on its own stream when torch's is the null stream:
+            # order the copies explicitly)
             eng.gram_upper_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), Ud.data_ptr())
+            eng.synchronize()
             Uh.copy_(Ud)
             tdist.all_reduce(Uh)
             Ud.copy_(Uh)
+            torch.cuda.synchronize()
             eng.finish_ptr(Ud.data_ptr(), X.data_ptr(), bdt, n, dl, X.stride(0), ff,
                            sel_t.data_ptr(), scores.data_ptr(), mean.data_ptr())
         else:

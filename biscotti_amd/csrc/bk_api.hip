@@ -94,6 +94,11 @@ struct bk_ctx {
     // reads them: an asynchronous caller learns of an invalid call there)
     int margin_unchecked = 0;
     double *hmargin = nullptr;  // pinned: the record, read back with the host outputs
+    // pinned: the n <= 128 host entries' outputs {margin, sel, scores, mean},
+    // read back in one copy (a D2H into pageable memory goes through HIP's
+    // staging: ~20 us per copy at config B)
+    void *hout = nullptr;
+    size_t hout_bytes = 0;
     // BK_F32_CERTIFIED: 1 while the exact re-run of a near-tie call is in progress
     int force_exact = 0;
     int64_t certified_reruns = 0;
@@ -788,28 +793,36 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
                                     (size_t)d * 8, (size_t)n, hipMemcpyDeviceToHost, c->stream));
         dX = c->X.p;
     }
-    CHK(ensure(c->sel, (size_t)n * sizeof(int64_t)));
-    CHK(ensure(c->scores, (size_t)n * sizeof(double)));
-    if (mean_out) CHK(ensure(c->mean, (size_t)d * sizeof(double)));
-    int64_t *dsel = (int64_t *)c->sel.p;
-    double *dsc = (double *)c->scores.p;
-    double *dmean = mean_out ? (double *)c->mean.p : nullptr;
+    // the outputs sit right behind the margin record in one device block
+    // {margin (16 doubles), sel (n), scores (n), mean (d)}, read back with ONE
+    // copy into pinned memory, then copied to the caller's arrays on the host
+    constexpr size_t MPAD = 16;
+    const size_t words = MPAD + 2 * (size_t)n + (mean_out ? (size_t)d : 0);
+    CHK(ensure(c->margin, words * sizeof(double)));
+    if (c->hout_bytes < words * sizeof(double)) {
+        if (c->hout) (void)hipHostFree(c->hout);
+        c->hout = nullptr;
+        c->hout_bytes = 0;
+        HIPCHK(hipHostMalloc(&c->hout, words * sizeof(double), hipHostMallocPortable));
+        c->hout_bytes = words * sizeof(double);
+    }
+    double *blk = (double *)c->margin.p;
+    int64_t *dsel = (int64_t *)(blk + MPAD);
+    double *dsc = blk + MPAD + n;
+    double *dmean = mean_out ? blk + MPAD + 2 * n : nullptr;
     CHK(run_small(c, dX, dtype, n, d, dld, f, dsel, dsc, dmean));
     CHK(timed(c, BK_K_D2H, [&] {
-        hipError_t e = hipMemcpyAsync(sel_idx, dsel, (size_t)m * sizeof(int64_t),
-                                      hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess && scores)
-            e = hipMemcpyAsync(scores, dsc, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
-                               c->stream);
-        if (e == hipSuccess && mean_out)
-            e = hipMemcpyAsync(mean_out, dmean, (size_t)d * sizeof(double), hipMemcpyDeviceToHost,
-                               c->stream);
-        return e;
+        return hipMemcpyAsync(c->hout, blk, words * sizeof(double), hipMemcpyDeviceToHost,
+                              c->stream);
     }));
-    CHK(queue_margin_readback(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     drain.armed = false;
-    CHK(check_margin_readback(c));
+    const double *h = (const double *)c->hout;
+    c->margin_unchecked = 0;
+    CHK(margin_status(h));
+    memcpy(sel_idx, h + MPAD, (size_t)m * sizeof(int64_t));
+    if (scores) memcpy(scores, h + MPAD + n, (size_t)n * sizeof(double));
+    if (mean_out) memcpy(mean_out, h + MPAD + 2 * n, (size_t)d * sizeof(double));
     if (m_out) *m_out = m;
     return BK_OK;
 }
@@ -936,6 +949,7 @@ void bk_destroy(bk_ctx *c) {
                           &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
                           &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws};
         if (c->hmargin) (void)hipHostFree(c->hmargin);
+        if (c->hout) (void)hipHostFree(c->hout);
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
