@@ -382,6 +382,20 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
                                                          dl.data_ptr(), nr, dr, rs.data_ptr())),
                       None, "RONI scores of %d updates on a %d x %d validation set "
                             "(logistic_validator.py:22-33)" % (nr, nv, dr))
+    # the torch-path RONI (K8, the mnist softmax verifier, ML/Pytorch/client_obj.py:100-112):
+    # a 6,000-sample shard of 784 fp32 pixels, 10 classes, 100 updates of 7,850
+    nvm, dinm, cm, nrm = 6000, 784, 10, 100
+    Xm = torch.randn((nvm, dinm), dtype=torch.float32, device=dev, generator=g2)
+    ym = torch.randint(0, cm, (nvm,), dtype=torch.int32, device=dev, generator=g2)
+    wm = torch.randn(cm * (dinm + 1), dtype=torch.float64, device=dev, generator=g2) * 0.05
+    dm = torch.randn((nrm, cm * (dinm + 1)), dtype=torch.float64, device=dev, generator=g2) * 1e-3
+    rsm = torch.empty(nrm, dtype=torch.float64, device=dev)
+    runs["k_roni_softmax"] = (
+        lambda: check(lib().bk_roni_softmax_device(eng.ctx, Xm.data_ptr(), nvm, dinm, dinm,
+                                                   ym.data_ptr(), cm, wm.data_ptr(), dm.data_ptr(),
+                                                   nrm, cm * (dinm + 1), rsm.data_ptr())),
+        None, "softmax RONI scores of %d updates (d = %d) on %d x %d fp32 samples, %d classes "
+              "(ML/Pytorch/client_obj.py:100-112)" % (nrm, cm * (dinm + 1), nvm, dinm, cm))
     res = {}
     for name, (fn, nbytes, what) in runs.items():
         fn()
@@ -390,9 +404,17 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
         for _ in range(steps):
             fn()
         torch.cuda.synchronize()
-        t = eng.timing_read().get(name)
+        t = eng.timing_read().get("k_roni" if name.startswith("k_roni") else name)
         eng.timing_enable(False)
         ms = t["avg_ms"]
+        if name == "k_roni_softmax":  # fp64 VALU FMAs: nv x (n+1) x C x d_in
+            fl = 2.0 * nvm * (nrm + 1) * cm * dinm
+            res[name] = {"what": what, "ms": round(ms, 4),
+                         "updates_per_s": round(nrm / (ms * 1e-3), 1),
+                         "fp64_tflops": round(fl / (ms * 1e-3) / 1e12, 3),
+                         "roofline": {"bound": "valu", "peak": 78.6, "unit": "TFLOP/s",
+                                      "frac": round(fl / (ms * 1e-3) / 1e12 / 78.6, 4)}}
+            continue
         if nbytes is None:  # RONI: latency / L2-bound, reported as a rate
             res[name] = {"what": what, "ms": round(ms, 4),
                          "updates_per_s": round(nr / (ms * 1e-3), 1),

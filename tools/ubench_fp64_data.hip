@@ -16,6 +16,8 @@
 //             config E's exact path)
 //   lds64   : rand64 operands re-read from LDS by ds_read_b128 at K1's rate
 //             (one 16-B granule per 4 MFMAs per operand side)
+//   rand64_2w, lds64_2w : the same with two waves per SIMD (512 threads, K1's
+//             occupancy)
 //
 // hipcc --offload-arch=gfx950 -O3 tools/ubench_fp64_data.hip -o tools/ubench_fp64_data
 #include <hip/hip_runtime.h>
@@ -41,13 +43,13 @@ typedef double d2v __attribute__((ext_vector_type(2)));
 constexpr int NOP = 16;  // operand values cycled per lane (registers)
 
 // MODE 0: operands from registers (cycled), 1: re-read from LDS each k-step
-template <int MODE>
-__global__ __launch_bounds__(256, 1) void k_mfma(const double *__restrict__ src, int iters,
-                                                 double *__restrict__ out,
-                                                 long long *__restrict__ clk) {
-    __shared__ __attribute__((aligned(16))) double lds[4][2][64 * 8];  // per wave: A, B images
+template <int MODE, int NT>
+__global__ __launch_bounds__(NT, 1) void k_mfma(const double *__restrict__ src, int iters,
+                                                double *__restrict__ out,
+                                                long long *__restrict__ clk) {
+    __shared__ __attribute__((aligned(16))) double lds[NT / 64][2][64 * 8];  // per wave: A, B
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const double *s = src + ((size_t)blockIdx.x * 256 + threadIdx.x) * 2 * NOP;
+    const double *s = src + ((size_t)blockIdx.x * NT + threadIdx.x) * 2 * NOP;
     double a[NOP], b[NOP];
 #pragma unroll
     for (int i = 0; i < NOP; ++i) {
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(256, 1) void k_mfma(const double *__restrict__ src,
     double t = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
-    out[(size_t)blockIdx.x * 256 + threadIdx.x] = t;
+    out[(size_t)blockIdx.x * NT + threadIdx.x] = t;
     if (threadIdx.x == 0) {
         clk[2 * blockIdx.x] = m1 - m0;
         clk[2 * blockIdx.x + 1] = r1 - r0;
@@ -118,18 +120,19 @@ int main(int argc, char **argv) {
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int ncu = prop.multiProcessorCount, grid = ncu;  // one 4-wave workgroup per CU
-    const size_t nop = (size_t)grid * 256 * 2 * NOP;
+    const size_t nop = (size_t)grid * 512 * 2 * NOP;
     std::vector<double> h(nop);
     double *dsrc, *dout;
     long long *dclk;
     CK(hipMalloc(&dsrc, nop * sizeof(double)));
-    CK(hipMalloc(&dout, (size_t)grid * 256 * sizeof(double)));
+    CK(hipMalloc(&dout, (size_t)grid * 512 * sizeof(double)));
     CK(hipMalloc(&dclk, (size_t)grid * 2 * sizeof(long long)));
     std::vector<long long> hc((size_t)grid * 2);
     const int iters = 250;  // 250 x 256 = 64,000 MFMAs per wave per launch
-    const char *names[] = {"const", "rand64", "rand32w", "lds64"};
+    const char *names[] = {"const", "rand64", "rand32w", "lds64", "rand64_2w", "lds64_2w"};
     printf("{\"cus\": %d, \"results\": [", ncu);
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < 6; ++v) {
+        const int nt = v >= 4 ? 512 : 256;  // waves per CU: 4 (one per SIMD) or 8
         for (size_t i = 0; i < nop; ++i) {
             const uint64_t r = sm64(i * 7919 + 12345);
             const double u = (double)(r >> 11) * 0x1p-53;  // [0, 1): full mantissa
@@ -141,9 +144,13 @@ int main(int argc, char **argv) {
         CK(hipMemcpy(dsrc, h.data(), nop * sizeof(double), hipMemcpyHostToDevice));
         auto launch = [&] {
             if (v == 3)
-                hipLaunchKernelGGL(k_mfma<1>, dim3(grid), dim3(256), 0, 0, dsrc, iters, dout, dclk);
+                hipLaunchKernelGGL((k_mfma<1, 256>), dim3(grid), dim3(256), 0, 0, dsrc, iters, dout, dclk);
+            else if (v == 4)
+                hipLaunchKernelGGL((k_mfma<0, 512>), dim3(grid), dim3(512), 0, 0, dsrc, iters, dout, dclk);
+            else if (v == 5)
+                hipLaunchKernelGGL((k_mfma<1, 512>), dim3(grid), dim3(512), 0, 0, dsrc, iters, dout, dclk);
             else
-                hipLaunchKernelGGL(k_mfma<0>, dim3(grid), dim3(256), 0, 0, dsrc, iters, dout, dclk);
+                hipLaunchKernelGGL((k_mfma<0, 256>), dim3(grid), dim3(256), 0, 0, dsrc, iters, dout, dclk);
         };
         launch();
         CK(hipDeviceSynchronize());
@@ -152,7 +159,7 @@ int main(int argc, char **argv) {
         CK(hipEventCreate(&e1));
         // back-to-back launches for `seconds` (warm: the clock settles), then
         // a timed window of 50 launches
-        const double flop_per_launch = (double)grid * 4 * iters * 256 * 2048.0;
+        const double flop_per_launch = (double)grid * (nt / 64) * iters * 256 * 2048.0;
         float ms = 0;
         CK(hipEventRecord(e0));
         launch();
