@@ -559,7 +559,11 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
         }
     }
     auto issue = [&](int64_t kb, int stage) {
+#ifdef BK_K1_L2WINDOW  // timing-only ablation: every k-block read from the first W (L2-resident)
+        const int64_t col = (kb % BK_K1_L2WINDOW) * BKE;
+#else
         const int64_t col = kb * BKE;
+#endif
         char *base = lds + stage * G3_STAGE;
 #ifndef BK_K1_GLDS_LIMIT  // timing-only ablation: issue at most this many glds per wave
 #define BK_K1_GLDS_LIMIT G3_MAXB

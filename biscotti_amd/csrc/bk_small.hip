@@ -494,21 +494,24 @@ __device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid,
     }
     __syncthreads();
     const uint64_t key = kbuf[e];
+    // each half compares against NP / 2 keys: the keys past NP (padding)
+    // never precede a real one, so the real keys' positions are unchanged
+    constexpr int HK = 8 * NB;
     int cnt = 0;
 #pragma unroll
-    for (int j0 = 0; j0 < 64; j0 += 8) {
+    for (int j0 = 0; j0 < HK; j0 += 8) {
         uint64_t o[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) o[u] = kbuf[64 * h + j0 + u];
+        for (int u = 0; u < 8; ++u) o[u] = kbuf[HK * h + j0 + u];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int j = 64 * h + j0 + u;
+            const int j = HK * h + j0 + u;
             cnt += (o[u] < key) || (o[u] == key && j < e);
         }
     }
     if (h == 1) rk[e] = cnt;
     __syncthreads();
-    if (h == 0) sbuf[cnt + rk[e]] = dkey_inv(key);
+    if (h == 0 && e < 2 * HK) sbuf[cnt + rk[e]] = dkey_inv(key);
     __syncthreads();
     stamp(tr, 1);
     double acc = 0.0;
@@ -571,19 +574,20 @@ __device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int tid, i
     __syncthreads();
     stamp(tr, 0);
     // rank of row e in the (score, index) total order: threads e and 128 + e
-    // count over the two halves of the 128 (padded) keys -- a fixed trip
-    // count, every LDS read issued ahead, no branch
+    // count over the two halves of the NP = 16 NB (padded) keys -- a fixed
+    // trip count, every LDS read issued ahead, no branch
     const int e = tid & 127, h = tid >> 7;
     const uint64_t ki = keys[e];
+    constexpr int HK = 8 * NB;  // halves of the NP = 16 NB keys (n <= NP: no real key past them)
     int cnt = 0;
 #pragma unroll
-    for (int j0 = 0; j0 < 64; j0 += 8) {
+    for (int j0 = 0; j0 < HK; j0 += 8) {
         uint64_t o[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) o[u] = keys[64 * h + j0 + u];
+        for (int u = 0; u < 8; ++u) o[u] = keys[HK * h + j0 + u];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int j = 64 * h + j0 + u;
+            const int j = HK * h + j0 + u;
             cnt += (o[u] < ki) || (o[u] == ki && j < e);
         }
     }
