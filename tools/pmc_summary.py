@@ -20,7 +20,9 @@ import sys
 
 # coalesced streaming readers (128-B requests tallied at 64 B): 16 B/lane, and
 # k_qsum's 8 B/lane (calibrated: doubled it equals m*d*8 exactly)
-WIDE_READS = ("k_gram3", "k_mean", "k_gram<", "k_noise", "k_qsum")
+WIDE_READS = ("k_gram3", "k_mean", "k_gram<", "k_noise", "k_qsum", "k_small")
+# the roofline kernel: K1, or the one-launch path for n <= 128 (configs A, B)
+K1_NAMES = ("k_gram", "k_small")
 
 
 def short(name):
@@ -124,8 +126,8 @@ def main():
     # K1 of the workload only: its dispatches within 2x of the longest k_gram
     # dispatch of each pass (bench.py also runs config B's chain, 500 launches
     # of ~20 us on the same grid, which an all-dispatch mean would average in)
-    big = load_pmc(prof, only=lambda k, t, tmax: not k.startswith("k_gram") or t >= 0.5 * tmax)
-    k1p = next((k for k in big if k.startswith("k_gram") and "FETCH_SIZE" in big[k]), None)
+    big = load_pmc(prof, only=lambda k, t, tmax: not k.startswith(K1_NAMES) or t >= 0.5 * tmax)
+    k1p = next((k for k in big if k.startswith(K1_NAMES) and "FETCH_SIZE" in big[k]), None)
     if k1p:
         c = big[k1p]
         gui = c.get("GRBM_GUI_ACTIVE", 0.0)
@@ -146,7 +148,7 @@ def main():
                                                       pmc_k1["pmc_dispatch_ms_mean"], rd + wr, rd, wr,
                                                       pmc_k1["tcc_hit_pct"], pmc_k1["mfma_busy_pct"],
                                                       pmc_k1["clock_ghz"])]
-    k1 = next((k for k in res if k.startswith("k_gram")), None)
+    k1 = next((k for k in res if k.startswith(K1_NAMES)), None)
     out_json = {"workload": workload, "source": prof, "kernels": res}
     if k1:
         out_json["k_gram"] = dict(res[k1])
