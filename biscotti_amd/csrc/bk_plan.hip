@@ -304,7 +304,25 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
     typedef std::vector<std::vector<std::vector<Seg>>> Lists;
     auto build_lists = [&](int rounds, Lists &lists) {
         lists.assign(NX, {});
-        if (mode == 2) {
+        if (mode == 3 && per_xcd % ng == 0) {
+            // aligned pieces: every group gets per_xcd / ng CUs of the XCD and
+            // the same k-block pieces, so the q-th CUs of all groups stream the
+            // same columns together and the row-blocks the groups share are
+            // read from HBM once and then from L2 (at the price of the groups'
+            // cost ratio in fill)
+            const int pg = per_xcd / ng;
+            for (int x = 0; x < NX; ++x)
+                for (int r = 0; r < rounds; ++r) {
+                    const int64_t span = K[x + 1] - K[x];
+                    const int64_t k0 = K[x] + span * r / rounds, k1 = K[x] + span * (r + 1) / rounds;
+                    for (int q = 0; q < pg; ++q)
+                        for (int g = 0; g < ng; ++g)
+                            lists[x].push_back({Seg{g, (int)(k0 + (k1 - k0) * q / pg), 1,
+                                                    (int)(k0 + (k1 - k0) * (q + 1) / pg), 0}});
+                }
+            return std::vector<int>(ng, 0);
+        }
+        if (mode == 2 || mode == 3) {
             for (int x = 0; x < NX; ++x)
                 for (int r = 0; r < rounds; ++r) {
                     const int64_t span = K[x + 1] - K[x];
@@ -410,7 +428,7 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
             H.seg.push_back(cnt);  // 0: an idle workgroup keeps b = 8 j + x
         }
     for (int g = 0; g < ng; ++g) {
-        G[g].Q = mode == 2 ? 0 : bestQ[g] * (mode == 1 ? bestR : 1);
+        G[g].Q = mode >= 2 ? 0 : bestQ[g] * (mode == 1 ? bestR : 1);
         G[g].wg0 = (int)H.wglist.size();
         H.wglist.insert(H.wglist.end(), gw[g].begin(), gw[g].end());
     }

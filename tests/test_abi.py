@@ -85,13 +85,17 @@ def test_plan_fills_the_chip():
     assert v[0].value == 4  # two band quads + two off-diagonal pairs of super-tiles
 
 
-@pytest.mark.parametrize("mode", ["2", "1", "0"])
-def test_plan_covers_every_kblock_once(mode, monkeypatch):
+@pytest.mark.parametrize("mode,rounds", [("2", ""), ("1", ""), ("0", ""), ("3", ""), ("3", "4"),
+                                         ("2", "8")])
+def test_plan_covers_every_kblock_once(mode, rounds, monkeypatch):
     """The planner's own check (bk_plan.hip): every (group, k-block) pair is
     owned by exactly one workgroup and every group has one ragged-tail
-    workgroup -- for McNaughton pieces (default), the v8 round-aligned strides
-    and the v7 interleave (BK_PLAN_MODE), over shapes from tiny to BK_MAX_N."""
+    workgroup -- for McNaughton pieces (default), the v8 round-aligned strides,
+    the v7 interleave and the aligned pieces (BK_PLAN_MODE), over shapes from
+    tiny to BK_MAX_N."""
     monkeypatch.setenv("BK_PLAN_MODE", mode)
+    if rounds:
+        monkeypatch.setenv("BK_PLAN_ROUNDS", rounds)
     L = _lib.lib()
     v = [ctypes.c_int64() for _ in range(4)]
     for n, d in [(1, 1), (2, 16), (65, 100), (100, 7850), (300, 1000003), (512, 1 << 20),
