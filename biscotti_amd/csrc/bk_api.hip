@@ -772,9 +772,12 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
         CHK(ensure(c->X, (size_t)n * dld * es));
         if (k > 0) CHK(ensure(c->noise, (size_t)n * k * d * sizeof(double)));
         CHK(timed(c, BK_K_H2D, [&] {
-            hipError_t e = hipMemcpy2DAsync(c->X.p, (size_t)dld * es, X, (size_t)ld * es,
-                                            (size_t)d * es, (size_t)n, hipMemcpyHostToDevice,
-                                            c->stream);
+            // rows already 16-B multiples (d even for fp64): one linear copy
+            hipError_t e = ld == dld ? hipMemcpyAsync(c->X.p, X, (size_t)n * d * es,
+                                                      hipMemcpyHostToDevice, c->stream)
+                                     : hipMemcpy2DAsync(c->X.p, (size_t)dld * es, X,
+                                                        (size_t)ld * es, (size_t)d * es, (size_t)n,
+                                                        hipMemcpyHostToDevice, c->stream);
             if (e == hipSuccess && k > 0)
                 e = hipMemcpy2DAsync(c->noise.p, (size_t)d * 8, noise, (size_t)noise_ld * 8,
                                      (size_t)d * 8, (size_t)(n * k), hipMemcpyHostToDevice,

@@ -64,6 +64,15 @@ static_assert(C_LINES * 32 == SMALL_CTR_WORDS, "bk_internal.h SMALL_CTR_WORDS");
 constexpr int SMALL_KC = BK_SMALL_KC;  // columns per chunk (groups of 8)
 constexpr int SMALL_GR = SMALL_KC / 2;  // 16-B granules per staged row
 constexpr int SMALL_SPLIT = 4;          // G items per chunk (each: a quarter of the blocks)
+#ifndef BK_SMALL_NT
+#define BK_SMALL_NT 256
+#endif
+// threads per k_small workgroup: 256 (one wave per SIMD) or 512 (two: the
+// MFMA pipe issues back to back only from two waves, tools/ubench_fp64_data:
+// 71 vs 77 TF/s, and the rank loops split over four threads per key)
+constexpr int SMALL_NT = BK_SMALL_NT;
+constexpr int SMALL_NW = SMALL_NT / 64;  // waves per workgroup
+static_assert(SMALL_NT == 256 || SMALL_NT == 512, "k_small runs 4 or 8 waves");
 
 // G item it -> (chunk c, part h).  The SPLIT parts of a chunk are items 8
 // apart, so under the static first assignment (workgroup b runs item b;
@@ -213,20 +222,21 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 // sub-step S (0: columns 2g, 1: 2g+1) of this wave's blocks J.. per 8-column
 // group; block positions are compile-time, so the fragments stay in registers
-template <int NB, int W, int S, int J, int NJ>
+template <int NB, int W, int S, int J, int NJ, int NW>
 __device__ __forceinline__ void small_mma_s(d4 *acc, const d2v (&fr)[NB]) {
     if constexpr (J < NJ) {
-        constexpr int b = W + 4 * J;
+        constexpr int b = W + NW * J;
         constexpr int bi = blk_bi(b, NB), bj = blk_bj(b, NB);
         acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[bi][S], fr[bj][S], acc[J], 0, 0, 0);
-        small_mma_s<NB, W, S, J + 1, NJ>(acc, fr);
+        small_mma_s<NB, W, S, J + 1, NJ, NW>(acc, fr);
     }
 }
-// both sub-steps, blocks interleaved: consecutive MFMAs never share an accumulator
-template <int NB, int W, int J, int NJ>
+// both sub-steps, blocks interleaved: consecutive MFMAs never share an
+// accumulator; wave W of NW owns blocks W, W + NW, ...
+template <int NB, int W, int J, int NJ, int NW>
 __device__ __forceinline__ void small_mma(d4 *acc, const d2v (&fr)[NB]) {
-    small_mma_s<NB, W, 0, J, NJ>(acc, fr);
-    small_mma_s<NB, W, 1, J, NJ>(acc, fr);
+    small_mma_s<NB, W, 0, J, NJ, NW>(acc, fr);
+    small_mma_s<NB, W, 1, J, NJ, NW>(acc, fr);
 }
 
 // 2 consecutive elements as fp64; VEC: one 16-B (fp64) / 8-B (fp32) load,
@@ -256,17 +266,17 @@ __device__ __forceinline__ int sg_off(int row, int gran) {
     return row * (SMALL_GR * 16) + ((gran ^ (row & (SMALL_GR - 1))) << 4);
 }
 
-template <typename T, bool VEC, int NB>
+template <typename T, bool VEC, int NB, int NT = SMALL_NT>
 struct SmallStage {
     static constexpr int ROWS = 16 * NB;
-    static constexpr int PER = (ROWS * SMALL_GR + 255) / 256;  // 16-B granules per thread
+    static constexpr int PER = (ROWS * SMALL_GR + NT - 1) / NT;  // 16-B granules per thread
     d2v v[PER];
     // every load of the item in flight at once (coalesced rows)
     __device__ __forceinline__ void load(const SmallArgs &a, int s, int tid) {
         const T *X = (const T *)a.X;
         const int64_t c0 = (int64_t)s * SMALL_KC;
         const int len = (int)(c0 + SMALL_KC < a.d ? SMALL_KC : a.d - c0);
-        static_assert(PER * 256 == ROWS * SMALL_GR, "every thread stages PER whole granules");
+        static_assert(PER * NT == ROWS * SMALL_GR, "every thread stages PER whole granules");
         const int len2 = len & ~1;  // whole column pairs of this chunk (KC but for the last)
         if (VEC && len2 >= 2) {
             // ONE code path for full chunks and the ragged last one: 16-B loads
@@ -277,7 +287,7 @@ struct SmallStage {
             // waits for the last item
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
-                const int gidx = tid + 256 * q;
+                const int gidx = tid + NT * q;
                 const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
                 const T *p = X + (int64_t)min(row, a.n - 1) * a.ld + c0;
                 const d2v pr = sm_ld2<T, true>(p + (col < len2 ? col : len2 - 2));
@@ -286,7 +296,7 @@ struct SmallStage {
             if (len & 1) {  // an odd ragged chunk: its last column (rare)
 #pragma unroll
                 for (int q = 0; q < PER; ++q) {
-                    const int gidx = tid + 256 * q;
+                    const int gidx = tid + NT * q;
                     const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
                     if (col == len - 1) v[q].x = (double)X[(int64_t)min(row, a.n - 1) * a.ld + c0 + col];
                 }
@@ -297,7 +307,7 @@ struct SmallStage {
         // columns, out-of-range ones zeroed by a select
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const int gidx = tid + 256 * q;
+            const int gidx = tid + NT * q;
             const int row = gidx / SMALL_GR, col = 2 * (gidx % SMALL_GR);
             const T *p = X + (int64_t)min(row, a.n - 1) * a.ld + c0;
             const double x0 = (double)p[col < len ? col : len - 1];
@@ -309,7 +319,7 @@ struct SmallStage {
     __device__ __forceinline__ void store(char *tile, int g0, int g1, int tid) {
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const int gidx = tid + 256 * q;
+            const int gidx = tid + NT * q;
             const int row = gidx / SMALL_GR, gr = gidx % SMALL_GR;
             if (gr >= g0 && gr < g1) *reinterpret_cast<d2v *>(tile + sg_off(row, gr)) = v[q];
         }
@@ -318,7 +328,7 @@ struct SmallStage {
 
 // the MFMAs of 8-column groups [t0, t1) of the staged tile, blocks J0 .. J1-1
 // of this wave's list
-template <int NB, int W, int J0, int J1>
+template <int NB, int W, int J0, int J1, int NW = SMALL_NW>
 __device__ __forceinline__ void small_gram_groups(d4 *acc, const char *tile, int lane, int t0,
                                                   int t1) {
     const int rr = lane & 15, g = lane >> 4;
@@ -330,7 +340,7 @@ __device__ __forceinline__ void small_gram_groups(d4 *acc, const char *tile, int
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb)
                 fr[rb] = *reinterpret_cast<const d2v *>(tile + sg_off(16 * rb + rr, 4 * t + g));
-            small_mma<NB, W, J0, J1>(acc, fr);
+            small_mma<NB, W, J0, J1, NW>(acc, fr);
         }
     }
 }
@@ -345,7 +355,7 @@ template <typename T, bool VEC, int NB, int W, int PART>
 __device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int c, long long *tr, int lane,
                                                 char *tile, SmallStage<T, VEC, NB> &st, double *wb) {
     constexpr int NBLK = NB * (NB + 1) / 2;
-    constexpr int NJ = (NBLK - W + 3) / 4;  // this wave's blocks
+    constexpr int NJ = (NBLK - W + SMALL_NW - 1) / SMALL_NW;  // this wave's blocks
     constexpr int J0 = PART * NJ / SMALL_SPLIT, J1 = (PART + 1) * NJ / SMALL_SPLIT;
     constexpr int NG = SMALL_KC / 8;
     const int rr = lane & 15, g = lane >> 4;
@@ -372,7 +382,7 @@ __device__ __forceinline__ void small_gram_wave(const SmallArgs &a, int c, long 
     double *sq = a.part + (int64_t)__builtin_amdgcn_readfirstlane(c) * (NP * NP + NP);
 #pragma unroll
     for (int j = J0; j < J1; ++j) {
-        const int b = W + 4 * j;
+        const int b = W + SMALL_NW * j;
         const int bi = blk_bi(b, NB), bj = blk_bj(b, NB);
 #pragma unroll
         for (int r = 0; r < 4; ++r) wb[(g + 4 * r) * 17 + rr] = (double)acc[j][r];
@@ -421,7 +431,15 @@ __device__ __forceinline__ void small_gram(const SmallArgs &a, int it, int wave,
     case 0: small_gram_w<T, VEC, NB, 0>(a, c, h, tr, lane, tile, st, wb); break;
     case 1: small_gram_w<T, VEC, NB, 1>(a, c, h, tr, lane, tile, st, wb); break;
     case 2: small_gram_w<T, VEC, NB, 2>(a, c, h, tr, lane, tile, st, wb); break;
+#if BK_SMALL_NT == 512
+    case 3: small_gram_w<T, VEC, NB, 3>(a, c, h, tr, lane, tile, st, wb); break;
+    case 4: small_gram_w<T, VEC, NB, 4>(a, c, h, tr, lane, tile, st, wb); break;
+    case 5: small_gram_w<T, VEC, NB, 5>(a, c, h, tr, lane, tile, st, wb); break;
+    case 6: small_gram_w<T, VEC, NB, 6>(a, c, h, tr, lane, tile, st, wb); break;
+    default: small_gram_w<T, VEC, NB, 7>(a, c, h, tr, lane, tile, st, wb); break;
+#else
     default: small_gram_w<T, VEC, NB, 3>(a, c, h, tr, lane, tile, st, wb); break;
+#endif
     }
 }
 
@@ -494,31 +512,36 @@ __device__ __forceinline__ void small_scores(const SmallArgs &a, int i, int tid,
     }
     __syncthreads();
     const uint64_t key = kbuf[e];
-    // each half compares against NP / 2 keys: the keys past NP (padding)
-    // never precede a real one, so the real keys' positions are unchanged
-    constexpr int HK = 8 * NB;
+    // the P2 = NT / 128 threads of key e each compare it against NP / P2
+    // keys: the keys past NP (padding) never precede a real one, so the real
+    // keys' positions are unchanged
+    constexpr int P2 = SMALL_NT / 128, HK = 16 * NB / P2, U = HK % 8 == 0 ? 8 : 4;
     int cnt = 0;
 #pragma unroll
-    for (int j0 = 0; j0 < HK; j0 += 8) {
-        uint64_t o[8];
+    for (int j0 = 0; j0 < HK; j0 += U) {
+        uint64_t o[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) o[u] = kbuf[HK * h + j0 + u];
+        for (int u = 0; u < U; ++u) o[u] = kbuf[HK * h + j0 + u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int j = HK * h + j0 + u;
             cnt += (o[u] < key) || (o[u] == key && j < e);
         }
     }
-    if (h == 1) rk[e] = cnt;
+    if (h >= 1) rk[(h - 1) * 128 + e] = cnt;
     __syncthreads();
-    if (h == 0 && e < 2 * HK) sbuf[cnt + rk[e]] = dkey_inv(key);
+    if (h == 0 && e < 16 * NB) {
+#pragma unroll
+        for (int q = 1; q < P2; ++q) cnt += rk[(q - 1) * 128 + e];
+        sbuf[cnt] = dkey_inv(key);
+    }
     __syncthreads();
     stamp(tr, 1);
     double acc = 0.0;
     if (1 + tid <= k && 1 + tid < 128) acc += sbuf[1 + tid];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-    if (lane == 0) red[wave] = acc;
+    if (lane == 0 && wave < 4) red[wave] = acc;  // K2's shape: 4 waves (any more hold +0.0)
     __syncthreads();
     if (tid == 0) {
         double sum = 0.0;
@@ -539,16 +562,17 @@ __device__ __forceinline__ void small_mean_stage(const SmallArgs &a, int c, int 
     const int cl = tid & 63, r0 = tid >> 6;
     const int64_t col = (int64_t)c * 64 + cl;
     const T *X = (const T *)a.X + (col < a.d ? col : a.d - 1);
-    // rows r0, r0 + 4, ... < 16 NB (rows past n repeat row n - 1: loads
+    // rows r0, r0 + NW, ... < 16 NB (rows past n repeat row n - 1: loads
     // without a guard, and the mean's mask never selects them)
-    double v[4 * NB];
+    constexpr int RU = 16 * NB / SMALL_NW;
+    double v[RU];
 #pragma unroll
-    for (int u = 0; u < 4 * NB; ++u) {
-        const int r = r0 + 4 * u;
+    for (int u = 0; u < RU; ++u) {
+        const int r = r0 + SMALL_NW * u;
         v[u] = (double)X[(int64_t)(r < a.n ? r : a.n - 1) * a.ld];
     }
 #pragma unroll
-    for (int u = 0; u < 4 * NB; ++u) cols[(r0 + 4 * u) * 64 + cl] = v[u];
+    for (int u = 0; u < RU; ++u) cols[(r0 + SMALL_NW * u) * 64 + cl] = v[u];
 }
 
 // M item c, part 2: every M item ranks the n published scores itself (n <=
@@ -578,24 +602,26 @@ __device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int tid, i
     // trip count, every LDS read issued ahead, no branch
     const int e = tid & 127, h = tid >> 7;
     const uint64_t ki = keys[e];
-    constexpr int HK = 8 * NB;  // halves of the NP = 16 NB keys (n <= NP: no real key past them)
+    // P2 parts of the NP = 16 NB keys (n <= NP: no real key past them)
+    constexpr int P2 = SMALL_NT / 128, HK = 16 * NB / P2, U = HK % 8 == 0 ? 8 : 4;
     int cnt = 0;
 #pragma unroll
-    for (int j0 = 0; j0 < HK; j0 += 8) {
-        uint64_t o[8];
+    for (int j0 = 0; j0 < HK; j0 += U) {
+        uint64_t o[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) o[u] = keys[HK * h + j0 + u];
+        for (int u = 0; u < U; ++u) o[u] = keys[HK * h + j0 + u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int j = HK * h + j0 + u;
             cnt += (o[u] < ki) || (o[u] == ki && j < e);
         }
     }
-    if (h == 1 && e < n) rkm[e] = cnt;
+    if (h >= 1 && e < n) rkm[(h - 1) * 128 + e] = cnt;
     __syncthreads();
     bool on = false;
     if (h == 0 && e < n) {
-        cnt += rkm[e];
+#pragma unroll
+        for (int q = 1; q < P2; ++q) cnt += rkm[(q - 1) * 128 + e];
         on = cnt < m;
         if (c == 0 && cnt == m - 1) bnd[0] = si;
         if (c == 0 && cnt == m) bnd[1] = si;
@@ -657,19 +683,19 @@ __device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int tid, i
 }
 
 template <typename T, bool VEC, int NB>
-__global__ __launch_bounds__(256) void k_small(SmallArgs a) {
+__global__ __launch_bounds__(SMALL_NT) void k_small(SmallArgs a) {
     __shared__ int s_item;
     __shared__ unsigned s_old;
     __shared__ __attribute__((aligned(16))) char tile[16 * NB * SMALL_GR * 16];  // G: rows x KC columns
     __shared__ uint64_t kbuf[128];                                      // S / selection keys
     __shared__ __attribute__((aligned(16))) double sbuf[128];          // S: the sorted row
-    __shared__ int rk[128];
+    __shared__ int rk[(SMALL_NT / 128 - 1) * 128];                      // partial ranks
     __shared__ double red[4];                                           // S waves
     __shared__ double bnd[2];
     __shared__ double dgl[128];
     __shared__ int srow[128];
     __shared__ uint64_t balw[2];
-    __shared__ double wbuf[4][16 * 17];  // G: each wave's block on its way out
+    __shared__ double wbuf[SMALL_NW][16 * 17];  // G: each wave's block on its way out
     static_assert(16 * NB * SMALL_GR * 16 >= 6 * 16 * NB * 8, "S items keep their sums in the tile");
     const int tid = threadIdx.x, wave = tid >> 6;
     const int NGI = SMALL_SPLIT * a.P;  // G items: SPLIT per chunk
@@ -771,7 +797,7 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
             __shared__ unsigned s_dirty;
             if (tid == 0) s_dirty = 0;
             __syncthreads();
-            for (int w = tid; w < C_LINES * 32; w += 256) {
+            for (int w = tid; w < C_LINES * 32; w += SMALL_NT) {
                 if ((w & 31) == 0) continue;
                 if (ctr_load(ctr + w) != 0u) {
                     __hip_atomic_store(ctr + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -812,14 +838,14 @@ __global__ __launch_bounds__(256) void k_tiny(SmallArgs a) {
     const int n = a.n, m = n - a.f;
     const int64_t k = n - a.f - 2 > 0 ? n - a.f - 2 : 0;
     {
-        SmallStage<T, VEC, 1> st;
+        SmallStage<T, VEC, 1, 256> st;
         st.load(a, 0, tid);
         st.store(tile, 0, SMALL_GR, tid);
     }
     __syncthreads();
     if (wave == 0) {
         d4 acc[1] = {d4{0.0, 0.0, 0.0, 0.0}};
-        small_gram_groups<1, 0, 0, 1>(acc, tile, lane, 0, SMALL_KC / 8);
+        small_gram_groups<1, 0, 0, 1, 4>(acc, tile, lane, 0, SMALL_KC / 8);
         const int rr = lane & 15, g = lane >> 4;
 #pragma unroll
         for (int r = 0; r < 4; ++r) gm[(g + 4 * r) * 17 + rr] = acc[0][r];
@@ -907,14 +933,14 @@ __global__ __launch_bounds__(256) void k_tiny(SmallArgs a) {
 template <typename T, bool VEC>
 static void launch_small_t(const SmallArgs &a, int NBv, int grid, hipStream_t st) {
     switch (NBv) {
-    case 1: hipLaunchKernelGGL((k_small<T, VEC, 1>), dim3(grid), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((k_small<T, VEC, 2>), dim3(grid), dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((k_small<T, VEC, 3>), dim3(grid), dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((k_small<T, VEC, 4>), dim3(grid), dim3(256), 0, st, a); break;
-    case 5: hipLaunchKernelGGL((k_small<T, VEC, 5>), dim3(grid), dim3(256), 0, st, a); break;
-    case 6: hipLaunchKernelGGL((k_small<T, VEC, 6>), dim3(grid), dim3(256), 0, st, a); break;
-    case 7: hipLaunchKernelGGL((k_small<T, VEC, 7>), dim3(grid), dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_small<T, VEC, 8>), dim3(grid), dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((k_small<T, VEC, 1>), dim3(grid), dim3(SMALL_NT), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_small<T, VEC, 2>), dim3(grid), dim3(SMALL_NT), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((k_small<T, VEC, 3>), dim3(grid), dim3(SMALL_NT), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_small<T, VEC, 4>), dim3(grid), dim3(SMALL_NT), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((k_small<T, VEC, 5>), dim3(grid), dim3(SMALL_NT), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((k_small<T, VEC, 6>), dim3(grid), dim3(SMALL_NT), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((k_small<T, VEC, 7>), dim3(grid), dim3(SMALL_NT), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_small<T, VEC, 8>), dim3(grid), dim3(SMALL_NT), 0, st, a); break;
     }
 }
 

@@ -7,6 +7,8 @@ if sys.argv[1] == "run":
     import torch
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from biscotti_amd import _lib
+    if os.environ.get("LIB"):  # another build, e.g. build_ab/libbk_nt512.so
+        _lib.LIB_PATH = os.path.abspath(os.environ["LIB"])
     from biscotti_amd.krum import Engine
     tf = os.environ["BK_SMALL_TRACE"]
     if os.path.exists(tf):
