@@ -97,8 +97,11 @@ struct bk_ctx {
     // pinned: the n <= 128 host entries' outputs {margin, sel, scores, mean},
     // read back in one copy (a D2H into pageable memory goes through HIP's
     // staging: ~20 us per copy at config B)
-    void *hout = nullptr;
+    void *hout = nullptr;  // the host small path's mapped output block (pinned, coherent)
     size_t hout_bytes = 0;
+    double *hout_dev = nullptr;          // its device address
+    const double *hout_host_margin = nullptr;  // its record, as the host reads it
+    const double *margin_host = nullptr;  // non-null: the last call's record is there
     // BK_F32_CERTIFIED: 1 while the exact re-run of a near-tie call is in progress
     int force_exact = 0;
     int64_t certified_reruns = 0;
@@ -473,6 +476,7 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
                               c->stream);
     }));
     c->margin_valid = 1;
+    c->margin_host = nullptr;
     c->margin_unchecked = 1;
     if (d_mean && d > 0) {
         double *seg = nullptr;
@@ -502,8 +506,11 @@ bool small_ok(const bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, 
     return c->small_on && n <= 128 && d <= dmax;
 }
 
+// margin_out / scores_out: the host entry's mapped output block (the record
+// and a second copy of the scores written by the kernel straight to host memory)
 int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld, int64_t f,
-              int64_t *d_sel, double *d_scores, double *d_mean) {
+              int64_t *d_sel, double *d_scores, double *d_mean, double *margin_out = nullptr,
+              double *scores_out = nullptr) {
     const SmallPlan sp = small_plan((int)n, d, c->num_cu);
     if (!c->small_ctr.p) {
         CHK(ensure(c->small_ctr, SMALL_CTR_WORDS * sizeof(unsigned)));
@@ -535,10 +542,12 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
     CHK(timed(c, BK_K_SMALL, [&] {
         return launch_small(dX, dtype, ld, (int)n, d, (int)f, sp, (double *)c->small_part.p,
                             (double *)c->U.p, sc, (double *)c->diag.p, d_sel, d_mean,
-                            (double *)c->margin.p, (unsigned *)c->small_ctr.p, c->num_cu,
-                            c->stream, trace, spin, c->small_check_lines);
+                            margin_out ? margin_out : (double *)c->margin.p,
+                            (unsigned *)c->small_ctr.p, c->num_cu, c->stream, trace, spin,
+                            c->small_check_lines, scores_out);
     }));
     c->margin_valid = 1;
+    c->margin_host = margin_out ? c->hout_host_margin : nullptr;
     c->margin_unchecked = 1;
     if (tfile) {
         std::vector<long long> h(twords + 6);
@@ -589,8 +598,13 @@ int margin_status(const double *mg) {
 // s_lo, s_hi, d, k, then u_G), synchronously
 int read_margin(bk_ctx *c, double (&mg)[MARGIN_WORDS]) {
     if (!c->margin_valid) return fail(BK_EINVAL, "no Multi-Krum call on this context yet");
-    HIPCHK(hipMemcpyAsync(mg, c->margin.p, sizeof mg, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->margin_host) {  // the host entry's record, written to host memory by the kernel
+        HIPCHK(hipStreamSynchronize(c->stream));
+        memcpy(mg, c->margin_host, sizeof mg);
+    } else {
+        HIPCHK(hipMemcpyAsync(mg, c->margin.p, sizeof mg, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     c->margin_unchecked = 0;
     return margin_status(mg);
 }
@@ -796,28 +810,38 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
                                     (size_t)d * 8, (size_t)n, hipMemcpyDeviceToHost, c->stream));
         dX = c->X.p;
     }
-    // the outputs sit right behind the margin record in one device block
-    // {margin (16 doubles), sel (n), scores (n), mean (d)}, read back with ONE
-    // copy into pinned memory, then copied to the caller's arrays on the host
+    // the outputs {margin (16 doubles), sel (n), scores (n), mean (d)} are
+    // written by the kernel itself into one mapped, coherent pinned block:
+    // no device-to-host copy after the kernel (a D2H costs ~15 us of PCIe
+    // round trip at config B, more than the 63 KB it moves), one synchronize,
+    // then copied to the caller's arrays on the host
     constexpr size_t MPAD = 16;
     const size_t words = MPAD + 2 * (size_t)n + (mean_out ? (size_t)d : 0);
-    CHK(ensure(c->margin, words * sizeof(double)));
     if (c->hout_bytes < words * sizeof(double)) {
         if (c->hout) (void)hipHostFree(c->hout);
         c->hout = nullptr;
         c->hout_bytes = 0;
-        HIPCHK(hipHostMalloc(&c->hout, words * sizeof(double), hipHostMallocPortable));
-        c->hout_bytes = words * sizeof(double);
+        c->hout_dev = nullptr;
+        c->hout_host_margin = nullptr;
+        c->margin_host = nullptr;
+        const size_t bytes = std::max<size_t>(words * sizeof(double), 64 * 1024);
+#ifdef BK_HOUT_NONCOHERENT  // ablation: GPU-cached host block (written back at kernel end)
+        const unsigned hflags = hipHostMallocPortable | hipHostMallocMapped | hipHostMallocNonCoherent;
+#else
+        const unsigned hflags = hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent;
+#endif
+        HIPCHK(hipHostMalloc(&c->hout, bytes, hflags));
+        c->hout_bytes = bytes;
+        void *dp = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dp, c->hout, 0));
+        c->hout_dev = (double *)dp;
+        c->hout_host_margin = (const double *)c->hout;
     }
-    double *blk = (double *)c->margin.p;
+    double *blk = c->hout_dev;
     int64_t *dsel = (int64_t *)(blk + MPAD);
-    double *dsc = blk + MPAD + n;
     double *dmean = mean_out ? blk + MPAD + 2 * n : nullptr;
-    CHK(run_small(c, dX, dtype, n, d, dld, f, dsel, dsc, dmean));
-    CHK(timed(c, BK_K_D2H, [&] {
-        return hipMemcpyAsync(c->hout, blk, words * sizeof(double), hipMemcpyDeviceToHost,
-                              c->stream);
-    }));
+    CHK(run_small(c, dX, dtype, n, d, dld, f, dsel, nullptr, dmean, blk,
+                  scores ? blk + MPAD + n : nullptr));
     HIPCHK(hipStreamSynchronize(c->stream));
     drain.armed = false;
     const double *h = (const double *)c->hout;

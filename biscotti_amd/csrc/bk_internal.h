@@ -150,7 +150,8 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
                         hipStream_t st, long long *trace = nullptr,
-                        uint64_t spin_max = SMALL_SPIN_MAX, int check_lines = 0);
+                        uint64_t spin_max = SMALL_SPIN_MAX, int check_lines = 0,
+                        double *scores_out = nullptr);
 hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, int64_t c0,
                         const int64_t *perm, const SynthParams &P, hipStream_t st);
 

@@ -65,7 +65,7 @@ constexpr int SMALL_KC = BK_SMALL_KC;  // columns per chunk (groups of 8)
 constexpr int SMALL_GR = SMALL_KC / 2;  // 16-B granules per staged row
 constexpr int SMALL_SPLIT = 4;          // G items per chunk (each: a quarter of the blocks)
 #ifndef BK_SMALL_NT
-#define BK_SMALL_NT 256
+#define BK_SMALL_NT 512
 #endif
 // threads per k_small workgroup: 256 (one wave per SIMD) or 512 (two: the
 // MFMA pipe issues back to back only from two waves, tools/ubench_fp64_data:
@@ -94,6 +94,7 @@ struct SmallArgs {
     int64_t ld, d;
     int n, f, kc, P, Q, nS, C, nblk, T;
     double *part, *U, *scores, *diag, *mean, *margin;
+    double *scores_out;  // optional second copy of the scores (the host entry's mapped block)
     int64_t *sel;
     unsigned *ctr;
     uint64_t spin_max;  // polls before a wait gives up (~1 s; a test knob lowers it)
@@ -625,6 +626,7 @@ __device__ __forceinline__ void small_mean(const SmallArgs &a, int c, int tid, i
         on = cnt < m;
         if (c == 0 && cnt == m - 1) bnd[0] = si;
         if (c == 0 && cnt == m) bnd[1] = si;
+        if (c == 0 && a.scores_out) a.scores_out[e] = si;
     }
     // compaction: rows 0..63 in wave 0, 64..127 in wave 1
     const uint64_t bal = __ballot(on);
@@ -970,8 +972,10 @@ SmallPlan small_plan(int n, int64_t d, int num_cu) {
 hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
-                        hipStream_t st, long long *trace, uint64_t spin_max, int check_lines) {
+                        hipStream_t st, long long *trace, uint64_t spin_max, int check_lines,
+                        double *scores_out) {
     SmallArgs a;
+    a.scores_out = scores_out;
     a.trace = trace;
     a.spin_max = spin_max;
     a.check_lines = check_lines;
@@ -999,6 +1003,7 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     const int grid = total < num_cu ? total : num_cu;
     const bool vec = (ld % 2) == 0 && ((uintptr_t)X % (dtype == 0 ? 16 : 8)) == 0;
     if (tiny_ok(n, d) && !trace) {  // one workgroup, no hand-offs (k_tiny)
+        if (scores_out) a.scores = scores_out;  // k_tiny never reads its scores back
         if (dtype == 0 && vec)
             hipLaunchKernelGGL((k_tiny<double, true>), dim3(1), dim3(256), 0, st, a);
         else if (dtype == 0)
