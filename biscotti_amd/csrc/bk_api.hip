@@ -97,7 +97,7 @@ struct bk_ctx {
     // pinned: the n <= 128 host entries' outputs {margin, sel, scores, mean},
     // read back in one copy (a D2H into pageable memory goes through HIP's
     // staging: ~20 us per copy at config B)
-    void *hout = nullptr;  // the host small path's mapped output block (pinned, coherent)
+    void *hout = nullptr;  // the host small path's mapped output block (pinned)
     size_t hout_bytes = 0;
     double *hout_dev = nullptr;          // its device address
     const double *hout_host_margin = nullptr;  // its record, as the host reads it
@@ -811,7 +811,7 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
         dX = c->X.p;
     }
     // the outputs {margin (16 doubles), sel (n), scores (n), mean (d)} are
-    // written by the kernel itself into one mapped, coherent pinned block:
+    // written by the kernel itself into one mapped pinned block:
     // no device-to-host copy after the kernel (a D2H costs ~15 us of PCIe
     // round trip at config B, more than the 63 KB it moves), one synchronize,
     // then copied to the caller's arrays on the host
@@ -825,10 +825,10 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
         c->hout_host_margin = nullptr;
         c->margin_host = nullptr;
         const size_t bytes = std::max<size_t>(words * sizeof(double), 64 * 1024);
-#ifdef BK_HOUT_NONCOHERENT  // ablation: GPU-cached host block (written back at kernel end)
-        const unsigned hflags = hipHostMallocPortable | hipHostMallocMapped | hipHostMallocNonCoherent;
-#else
+#ifdef BK_HOUT_COHERENT  // ablation: uncached host block (each store crosses PCIe at once)
         const unsigned hflags = hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent;
+#else  // GPU-cached, written back at the kernel's end: 156 vs 157 us per call at B
+        const unsigned hflags = hipHostMallocPortable | hipHostMallocMapped | hipHostMallocNonCoherent;
 #endif
         HIPCHK(hipHostMalloc(&c->hout, bytes, hflags));
         c->hout_bytes = bytes;

@@ -20,6 +20,10 @@ import bench  # noqa: E402
 from biscotti_amd.krum import Engine  # noqa: E402
 
 label = sys.argv[1] if len(sys.argv) > 1 else "host"
+# torch's HIP runtime first: torch ships its own libamdhip64, and when libbk's
+# (/opt/rocm) initialises the device first, torch's init then finds no GPU
+import torch  # noqa: E402
+torch.zeros(1, device="cuda")
 eng = Engine(0)
 r = bench.host_entry_variant(eng, "cuda:0", os.environ.get("WL", "B_mnist"),
                              single_calls=int(os.environ.get("SINGLE", 15)),
