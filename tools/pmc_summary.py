@@ -79,7 +79,11 @@ def load_pmc(d, only=None):
         res[k]["_dispatches"] = len(v)
     for k, v in clocks.items():
         v = sorted(v)
-        res[k]["_clock_ghz_median"] = v[len(v) // 2]
+        med = v[len(v) // 2]
+        # GRBM_GUI_ACTIVE spans the pass's counter window around the dispatch:
+        # for a ~20 us kernel (k_small) that window dwarfs the kernel and the
+        # ratio reads above the 2.4 GHz maximum -- no clock, not a wrong one
+        res[k]["_clock_ghz_median"] = med if med <= 2.45 else None
     return res
 
 
@@ -113,6 +117,7 @@ def main():
         # the clock from each dispatch's own duration in the PMC pass; the
         # all-call rocprof average mixes shapes (r1 reported an impossible 6.26 GHz)
         clk = c.get("_clock_ghz_median", float("nan"))
+        clk = float("nan") if clk is None else clk
         simd_cycles = gui / 8.0 * 1024 if gui else 0
         mb = 100.0 * busy / simd_cycles if simd_cycles else float("nan")
         res.setdefault(k, {}).update(fetch_kib=c["FETCH_SIZE"], read_bytes_corrected=rd,
@@ -139,15 +144,16 @@ def main():
                       hbm_bytes_per_launch=rd + wr,
                       tcc_hit_pct=100.0 * hit / (hit + miss) if hit + miss else float("nan"),
                       mfma_busy_pct=100.0 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / sc if sc else float("nan"),
-                      clock_ghz=c.get("_clock_ghz_median", float("nan")), fetch_correction=2.0,
+                      clock_ghz=c.get("_clock_ghz_median"), fetch_correction=2.0,
                       pmc_dispatch_ms_mean=c.get("_dispatch_ms_mean"),
                       pmc_dispatches=c.get("_dispatches"))
         lines += ["", "K1 of the workload only (%s dispatches >= half the longest of their pass; %d over the PMC passes, "
                   "mean %.3f ms): HBM bytes/launch %.4g (read %.4g corrected, write %.4g), TCC hit %.1f%%, "
-                  "MFMA busy %.1f%%, clock %.2f GHz" % (k1p, pmc_k1["pmc_dispatches"],
+                  "MFMA busy %.1f%%, clock %s GHz" % (k1p, pmc_k1["pmc_dispatches"],
                                                       pmc_k1["pmc_dispatch_ms_mean"], rd + wr, rd, wr,
                                                       pmc_k1["tcc_hit_pct"], pmc_k1["mfma_busy_pct"],
-                                                      pmc_k1["clock_ghz"])]
+                                                      "%.2f" % pmc_k1["clock_ghz"] if pmc_k1["clock_ghz"]
+                                                      else "n/a (kernel shorter than the counter window)")]
     k1 = next((k for k in res if k.startswith(K1_NAMES)), None)
     out_json = {"workload": workload, "source": prof, "kernels": res}
     if k1:
