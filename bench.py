@@ -526,6 +526,22 @@ def small_variant(eng, dev, name="B_mnist", steps=500, warmup=50):
                                         "frac": round(t_floor / ms, 4)},
                       "parity": golden_check(name, sel.cpu().numpy(), mean.cpu().numpy(), 0, d)}
     eng.set_small_path(True)
+    # the one kernel of the one-launch path (k_small, or k_tiny at A), evented
+    # on libbk's stream in a pass of its own: its HBM roofline over the
+    # algorithmic bytes of the call (the Gram's read of X and K4's read of the
+    # m selected rows, the mean's write) and its hash-matched PMC traffic
+    eng.timing_select(["k_small"])
+    for _ in range(max(50, steps // 5)):
+        step()
+    kt = eng.timing_read().get("k_small", {})
+    eng.timing_select([])
+    if kt.get("avg_ms"):
+        traffic, tsrc = pmc_traffic(name)
+        ach = bytes_alg / (kt["avg_ms"] * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "achieved": round(ach, 3), "peak": PEAK_HBM_GBS,
+                           "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic,
+                           "traffic_source": tsrc, "kernel": "k_tiny" if n <= 16 and d <= 128 else "k_small",
+                           "kernel_avg_ms": round(kt["avg_ms"], 5), "bytes_per_launch": bytes_alg}
     res["ms_per_step"] = res["one_launch"]["ms_per_step"]
     res["value"] = res["one_launch"]["GB_per_s"]
     del X

@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_run.sh "zc 120 ./tools/ubench_zc"
+bash tools/profile.sh A --workload A_creditcard --steps 500 --warmup 50 || exit $?
+bash tools/gpu_run.sh "bench 900 python bench.py"

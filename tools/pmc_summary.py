@@ -22,7 +22,7 @@ import sys
 # k_qsum's 8 B/lane (calibrated: doubled it equals m*d*8 exactly)
 WIDE_READS = ("k_gram3", "k_mean", "k_gram<", "k_noise", "k_qsum", "k_small")
 # the roofline kernel: K1, or the one-launch path for n <= 128 (configs A, B)
-K1_NAMES = ("k_gram", "k_small")
+K1_NAMES = ("k_gram", "k_small", "k_tiny")
 
 
 def short(name):
