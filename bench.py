@@ -967,8 +967,21 @@ def main():
                                                meanh.ctypes.data))
             ts.append(time.perf_counter() - t0)
         t = min(ts)
+        # the verifier's one call per batch after idle: the copy phase runs the
+        # chunks' K1s, so the clock ramp (single_call above) is paid under it
+        idle = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            time.sleep(0.2)
+            t0 = time.perf_counter()
+            _lib.check(_lib.lib().bk_multikrum(eng.ctx, ctypes.c_void_p(Xh.data_ptr()),
+                                               _lib.BK_HOST_PINNED, bdt, n, dl, dl, f,
+                                               selh.ctypes.data, ctypes.addressof(mo), None,
+                                               meanh.ctypes.data))
+            idle.append((time.perf_counter() - t0) * 1e3)
         out["e2e_pinned_h2d_d2h"] = {"GB_per_s": round(n * d * es / t / 1e9, 3),
                                      "ms": round(t * 1e3, 3),
+                                     "after_idle_ms": [round(x, 3) for x in idle],
                                      "selected_set_same": bool(np.array_equal(
                                          selh, sel.cpu().numpy()))}
         del Xh

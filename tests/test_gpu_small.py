@@ -153,3 +153,31 @@ def test_timing_stride_samples_launches(engine, oracle):
     finally:
         engine.timing_stride(1)
         engine.timing_select([])
+
+
+@pytest.mark.parametrize("n,d,f,dtype", [(100, 7850, 30, np.float64), (10, 25, 2, np.float64),
+                                         (128, 4097, 38, np.float64), (33, 1003, 10, np.float32)])
+def test_host_entry_writes_outputs_in_place(engine, oracle, n, d, f, dtype):
+    """The synchronous host entry at n <= 128: k_small / k_tiny write sel,
+    scores, mean and the margin record straight into a mapped pinned block
+    (no device-to-host copy).  Bitwise the device entry's outputs, the same
+    margin record, and bk_selection_margin follows whichever call was last."""
+    Xh = oracle.synth(n, d, 900 + n, max(1, f // 2), dtype=dtype)
+    other = oracle.synth(n, d, 901 + n, max(1, f // 2), dtype=dtype)
+    hs, hsc, hm = engine.multikrum(Xh, f)
+    hmg = engine.selection_margin()
+    ds, dsc, dm = _run(engine, torch.from_numpy(Xh).cuda(), f)
+    dmg = engine.selection_margin()
+    assert np.array_equal(hs, ds)
+    assert np.array_equal(hsc.view(np.uint8), dsc.view(np.uint8))
+    assert np.array_equal(hm.view(np.uint8), dm.view(np.uint8))
+    assert hmg == dmg
+    osel, _, _ = oracle.krum(Xh, f)
+    assert np.array_equal(hs, osel)
+    # a device call on another batch, then the host entry again: each margin
+    # read returns the last call's record, wherever it lives
+    _run(engine, torch.from_numpy(other).cuda(), f)
+    omg = engine.selection_margin()
+    engine.multikrum(Xh, f)
+    assert engine.selection_margin() == hmg
+    assert omg != hmg

@@ -137,14 +137,15 @@ def main():
         c = big[k1p]
         gui = c.get("GRBM_GUI_ACTIVE", 0.0)
         sc = gui / 8.0 * 1024 if gui else 0
-        rd = c["FETCH_SIZE"] * 1024.0 * 2.0
+        k1corr = 2.0 if any(w in k1p for w in WIDE_READS) else 1.0  # k_tiny: narrow loads
+        rd = c["FETCH_SIZE"] * 1024.0 * k1corr
         wr = c.get("WRITE_SIZE", 0.0) * 1024.0
         hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
         pmc_k1 = dict(fetch_kib=c["FETCH_SIZE"], read_bytes_corrected=rd, write_bytes=wr,
                       hbm_bytes_per_launch=rd + wr,
                       tcc_hit_pct=100.0 * hit / (hit + miss) if hit + miss else float("nan"),
                       mfma_busy_pct=100.0 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / sc if sc else float("nan"),
-                      clock_ghz=c.get("_clock_ghz_median"), fetch_correction=2.0,
+                      clock_ghz=c.get("_clock_ghz_median"), fetch_correction=k1corr,
                       pmc_dispatch_ms_mean=c.get("_dispatch_ms_mean"),
                       pmc_dispatches=c.get("_dispatches"))
         lines += ["", "K1 of the workload only (%s dispatches >= half the longest of their pass; %d over the PMC passes, "
