@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -93,6 +94,7 @@ struct bk_ctx {
     // a finish ran since its record's error codes were last read (bk_synchronize
     // reads them: an asynchronous caller learns of an invalid call there)
     int margin_unchecked = 0;
+    int64_t spin_us = 2000;  // wait_stream: poll this long before blocking (BK_SPIN_US)
     double *hmargin = nullptr;  // pinned: the record, read back with the host outputs
     // pinned: the n <= 128 host entries' outputs {margin, sel, scores, mean},
     // read back in one copy (a D2H into pageable memory goes through HIP's
@@ -580,6 +582,30 @@ int run_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
     return stage_finish(c, U, pl, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
 }
 
+// Wait for the context's stream: poll it for up to spin_us, then block.  A
+// blocking wait sleeps the host thread until the GPU's completion interrupt;
+// after the GPU has idled that wake-up was 40-75 us of a config-B call
+// (tools/idle_probe.py: device-resident call after 200 ms idle 152 -> 77 us,
+// host entry 229 -> 186 us, with the whole process set to spin).  Polling
+// only inside libbk's own waits keeps that without a process-wide flag, and
+// the cap bounds the CPU a long call (config D's 76 ms host entry) burns.
+// The final hipStreamSynchronize returns at once on a finished stream.
+hipError_t wait_stream(bk_ctx *c) {
+    if (c->spin_us > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const auto cap = std::chrono::microseconds(c->spin_us);
+        for (;;) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q != hipErrorNotReady) {
+                if (q != hipSuccess) return q;
+                break;
+            }
+            if (std::chrono::steady_clock::now() - t0 > cap) break;
+        }
+    }
+    return hipStreamSynchronize(c->stream);
+}
+
 // the error codes a finish can leave in margin[2] (bk_internal.h MARGIN_*)
 int margin_status(const double *mg) {
     if (mg[2] == MARGIN_HANDOFF_TIMEOUT)
@@ -599,11 +625,11 @@ int margin_status(const double *mg) {
 int read_margin(bk_ctx *c, double (&mg)[MARGIN_WORDS]) {
     if (!c->margin_valid) return fail(BK_EINVAL, "no Multi-Krum call on this context yet");
     if (c->margin_host) {  // the host entry's record, written to host memory by the kernel
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(wait_stream(c));
         memcpy(mg, c->margin_host, sizeof mg);
     } else {
         HIPCHK(hipMemcpyAsync(mg, c->margin.p, sizeof mg, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(wait_stream(c));
     }
     c->margin_unchecked = 0;
     return margin_status(mg);
@@ -757,7 +783,7 @@ int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
         return e;
     }));
     CHK(queue_margin_readback(c));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(wait_stream(c));
     drain.armed = false;
     CHK(check_margin_readback(c));
     if (m_out) *m_out = m;
@@ -842,7 +868,7 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
     double *dmean = mean_out ? blk + MPAD + 2 * n : nullptr;
     CHK(run_small(c, dX, dtype, n, d, dld, f, dsel, nullptr, dmean, blk,
                   scores ? blk + MPAD + n : nullptr));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(wait_stream(c));
     drain.armed = false;
     const double *h = (const double *)c->hout;
     c->margin_unchecked = 0;
@@ -930,6 +956,9 @@ int bk_create(bk_ctx **out, int device) {
     c->device = device;
     bind_epoch(c);
     DeviceGuard dg(device);
+    // probe knob: how the host waits for the GPU (hipDeviceScheduleSpin 1,
+    // Yield 2, BlockingSync 4; tools/idle_probe.py)
+    if (const char *v = getenv("BK_SCHED")) (void)hipSetDeviceFlags((unsigned)atoi(v));
     hipDeviceProp_t prop;
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e == hipSuccess) c->num_cu = prop.multiProcessorCount;
@@ -943,6 +972,7 @@ int bk_create(bk_ctx **out, int device) {
         if (strcmp(v, "v1") == 0) c->gram_variant = 1;
     if (const char *v = getenv("BK_GRAM_MODE")) c->gram_mode = atoi(v);
     if (const char *v = getenv("BK_SMALL")) c->small_on = atoi(v) != 0;
+    if (const char *v = getenv("BK_SPIN_US")) c->spin_us = atoll(v);
     // test / debug knobs (tests/test_gpu_errors.py): a hand-off wait that gives
     // up after this many polls; the queue-line invariant check; a sharded call
     // that fails before its exchange
@@ -1010,7 +1040,7 @@ int bk_synchronize(bk_ctx *c) {
     if (!c) return fail(BK_EINVAL, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(wait_stream(c));
     if (c->margin_unchecked) {  // the last finish's error codes (an asynchronous caller's only check)
         double mg[MARGIN_WORDS];
         CHK(read_margin(c, mg));

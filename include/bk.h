@@ -74,7 +74,8 @@ void bk_destroy(bk_ctx *ctx);
 /* Run on a caller stream (hipStream_t passed as void*); NULL = own stream. */
 int bk_set_stream(bk_ctx *ctx, void *hip_stream);
 void *bk_get_stream(bk_ctx *ctx);
-/* Waits for the context stream, then reports whether the last Multi-Krum call
+/* Waits for the context stream (polling it for up to BK_SPIN_US, default
+ * 2000 us, then blocking), then reports whether the last Multi-Krum call
  * on it produced valid outputs: BK_EHIP when k_small's hand-off wait gave up
  * (its sel entries are then -1), BK_ERCCL when a rank of a sharded call failed
  * before the exchange (bk_multikrum_sharded_device).  The asynchronous device
