@@ -7,6 +7,9 @@ medians printed as one JSON line.
   host       bk_multikrum(BK_HOST_PINNED): copy + kernel + outputs
   wake+host  a 1-element torch kernel, synchronize, then the host entry
              (does waking the GPU first help, and what does the wake cost?)
+  prewarm1ms_host  a tiny asynchronous Multi-Krum launch, 1 ms of sleep, then
+             the host entry (timed): a verifier waking the GPU as the first
+             update of a batch arrives
   warm_host  the host entry back to back (no idle), for scale
 
     python tools/idle_probe.py
@@ -67,15 +70,30 @@ def wake_host():
     host()
 
 
+Xt = torch.zeros((4, 8), dtype=torch.float64, device="cuda")
+selt = torch.empty(2, dtype=torch.int64, device="cuda")
+
+
+def prewarm_host():
+    # what a verifier could do when its first update arrives: one tiny
+    # asynchronous launch on the engine's stream, then the batch 1 ms later
+    # (the prewarm is outside the timed call, as it would be in the verifier)
+    eng.multikrum_device_ptr(Xt.data_ptr(), _lib.BK_F64, 4, 8, 8, 2, selt.data_ptr())
+    time.sleep(0.001)
+
+
 for _ in range(50):
     host()
     device()
 res = {}
-for name, fn in (("h2d", h2d), ("device", device), ("host", host), ("wake+host", wake_host)):
+for name, fn, pre in (("h2d", h2d, None), ("device", device, None), ("host", host, None),
+                      ("wake+host", wake_host, None), ("prewarm1ms_host", host, prewarm_host)):
     ts = []
     for _ in range(REPS):
         torch.cuda.synchronize()
         time.sleep(IDLE)
+        if pre:
+            pre()
         t0 = time.perf_counter()
         fn()
         ts.append((time.perf_counter() - t0) * 1e6)
