@@ -80,7 +80,7 @@ struct bk_ctx {
     // workspace (grow-only)
     DevBuf part, U, Ug, scores, mask, sel, X, mean, perm, trace, idx;
     // the selection margin of the last finish (K2 diag, K3 boundary scores, K3b record)
-    DevBuf diag, bnd, margin;
+    DevBuf diag, bnd;
     DevBuf Ut;  // K2 at large n: transposed off-diagonal tiles + diagonal (k_transpose)
     // k_small (n <= 128, one launch): its queue counters (zeroed once; every
     // launch leaves them zero) and the split-K partials
@@ -95,7 +95,11 @@ struct bk_ctx {
     // reads them: an asynchronous caller learns of an invalid call there)
     int margin_unchecked = 0;
     int64_t spin_us = 2000;  // wait_stream: poll this long before blocking (BK_SPIN_US)
-    double *hmargin = nullptr;  // pinned: the record, read back with the host outputs
+    // the record of the last finish, written by the kernels straight into mapped
+    // pinned memory (GPU-cached, written back at the kernel's end): the host
+    // reads it after the stream has finished, with no device-to-host copy
+    double *hmargin = nullptr;
+    double *dmargin = nullptr;  // its device address
     // pinned: the n <= 128 host entries' outputs {margin, sel, scores, mean},
     // read back in one copy (a D2H into pageable memory goes through HIP's
     // staging: ~20 us per copy at config B)
@@ -207,7 +211,7 @@ void bind_epoch(bk_ctx *c) {
     DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,   &c->scores, &c->mask,   &c->sel,
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                      &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
+                      &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
                       &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
@@ -437,6 +441,23 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
     return BK_OK;
 }
 
+// the context's mapped margin record (allocated once: never moves, so a
+// captured graph's pointer to it stays valid)
+int margin_rec(bk_ctx *c) {
+    if (c->hmargin) return BK_OK;
+    void *p = nullptr, *dp = nullptr;
+    HIPCHK(hipHostMalloc(&p, 128, hipHostMallocPortable | hipHostMallocMapped |
+                                      hipHostMallocNonCoherent));
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
+        (void)hipHostFree(p);
+        return fail(BK_EHIP, "hipHostGetDevicePointer of the margin record failed");
+    }
+    memset(p, 0, 128);
+    c->hmargin = (double *)p;
+    c->dmargin = (double *)dp;
+    return BK_OK;
+}
+
 // K2 + K3 + K4 from a packed upper Gram
 int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int dtype,
                  int64_t n, int64_t d, int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
@@ -449,7 +470,7 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     }
     CHK(ensure(c->diag, (size_t)n * sizeof(double)));
     CHK(ensure(c->bnd, 2 * sizeof(double)));
-    CHK(ensure(c->margin, MARGIN_WORDS * sizeof(double)));
+    CHK(margin_rec(c));
     int *mask = (int *)c->mask.p;
     double *diag = (double *)c->diag.p, *bnd = (double *)c->bnd.p;
     const int64_t m = n - f;
@@ -474,11 +495,10 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     CHK(timed(c, BK_K_RANK,
               [&] { return launch_rank(sc, (int)n, (int)m, mask, bnd, c->stream); }));
     CHK(timed(c, BK_K_COMPACT, [&] {
-        return launch_compact(mask, (int)n, d_sel, diag, bnd, dcols, k, (double *)c->margin.p,
-                              c->stream);
+        return launch_compact(mask, (int)n, d_sel, diag, bnd, dcols, k, c->dmargin, c->stream);
     }));
     c->margin_valid = 1;
-    c->margin_host = nullptr;
+    c->margin_host = c->hmargin;
     c->margin_unchecked = 1;
     if (d_mean && d > 0) {
         double *seg = nullptr;
@@ -523,7 +543,7 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
     CHK(ensure(c->small_part, (size_t)sp.P * (np16 * np16 + np16) * sizeof(double)));
     CHK(ensure(c->U, (size_t)bk_upper_elems(n) * sizeof(double)));
     CHK(ensure(c->diag, (size_t)n * sizeof(double)));
-    CHK(ensure(c->margin, MARGIN_WORDS * sizeof(double)));
+    CHK(margin_rec(c));
     double *sc = d_scores;
     if (!sc) {
         CHK(ensure(c->scores, (size_t)n * sizeof(double)));
@@ -544,12 +564,12 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
     CHK(timed(c, BK_K_SMALL, [&] {
         return launch_small(dX, dtype, ld, (int)n, d, (int)f, sp, (double *)c->small_part.p,
                             (double *)c->U.p, sc, (double *)c->diag.p, d_sel, d_mean,
-                            margin_out ? margin_out : (double *)c->margin.p,
+                            margin_out ? margin_out : c->dmargin,
                             (unsigned *)c->small_ctr.p, c->num_cu, c->stream, trace, spin,
                             c->small_check_lines, scores_out);
     }));
     c->margin_valid = 1;
-    c->margin_host = margin_out ? c->hout_host_margin : nullptr;
+    c->margin_host = margin_out ? c->hout_host_margin : c->hmargin;
     c->margin_unchecked = 1;
     if (tfile) {
         std::vector<long long> h(twords + 6);
@@ -623,33 +643,21 @@ int margin_status(const double *mg) {
 // the last finish's margin record (k_compact: gap, err_bound, near_tie, M,
 // s_lo, s_hi, d, k, then u_G), synchronously
 int read_margin(bk_ctx *c, double (&mg)[MARGIN_WORDS]) {
-    if (!c->margin_valid) return fail(BK_EINVAL, "no Multi-Krum call on this context yet");
-    if (c->margin_host) {  // the host entry's record, written to host memory by the kernel
-        HIPCHK(wait_stream(c));
-        memcpy(mg, c->margin_host, sizeof mg);
-    } else {
-        HIPCHK(hipMemcpyAsync(mg, c->margin.p, sizeof mg, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(wait_stream(c));
-    }
+    if (!c->margin_valid || !c->margin_host)
+        return fail(BK_EINVAL, "no Multi-Krum call on this context yet");
+    // the record sits in mapped host memory (the context's, or the n <= 128
+    // host entry's output block): once the stream is done it is readable
+    HIPCHK(wait_stream(c));
+    memcpy(mg, c->margin_host, sizeof mg);
     c->margin_unchecked = 0;
     return margin_status(mg);
 }
 
-// Synchronous host entries: the record comes back with the outputs (queued on
-// the stream before the caller's sync), and its error codes are checked
-int queue_margin_readback(bk_ctx *c) {
-    if (!c->hmargin) {
-        void *p = nullptr;
-        HIPCHK(hipHostMalloc(&p, MARGIN_WORDS * sizeof(double), hipHostMallocPortable));
-        c->hmargin = (double *)p;
-    }
-    HIPCHK(hipMemcpyAsync(c->hmargin, c->margin.p, MARGIN_WORDS * sizeof(double),
-                          hipMemcpyDeviceToHost, c->stream));
-    return BK_OK;
-}
-int check_margin_readback(bk_ctx *c) {  // after the stream has synchronized
+// Synchronous host entries: once their stream has synchronized, the record's
+// error codes are checked (it is already in host memory)
+int check_margin_readback(bk_ctx *c) {
     c->margin_unchecked = 0;
-    return margin_status(c->hmargin);
+    return margin_status(c->margin_host);
 }
 
 // Error paths of the host entries: queued H2D copies may still read the
@@ -782,7 +790,6 @@ int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
                                c->stream);
         return e;
     }));
-    CHK(queue_margin_readback(c));
     HIPCHK(wait_stream(c));
     drain.armed = false;
     CHK(check_margin_readback(c));
@@ -1003,7 +1010,7 @@ void bk_destroy(bk_ctx *c) {
         DevBuf *bufs[] = {&c->part, &c->U,    &c->Ug,  &c->scores,
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
-                          &c->noise, &c->diag, &c->bnd, &c->margin, &c->Ut, &c->small_ctr, &c->small_part,
+                          &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
                           &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws};
         if (c->hmargin) (void)hipHostFree(c->hmargin);
         if (c->hout) (void)hipHostFree(c->hout);
@@ -1799,7 +1806,6 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
                                    hipMemcpyDeviceToHost, c->stream);
             return e;
         }));
-        CHK(queue_margin_readback(c));
     }
     for (int r = 0; r < G; ++r) {
         DeviceGuard dg(g->ctx[(size_t)r]->device);
@@ -1813,7 +1819,7 @@ int bk_group_multikrum(bk_group *g, const void *X, int where, int dtype, int64_t
     // taken on the fp32 MFMA is re-run exact from the device-resident shards.
     // Every device holds the same summed record, so device 0's margin decides.
     bk_ctx *c0x = g->ctx[0];
-    if (certified(c0x, dtype) && c0x->hmargin[2] == 1.0 && c0x->hmargin[8] > 0x1p-53) {
+    if (certified(c0x, dtype) && c0x->margin_host[2] == 1.0 && c0x->margin_host[8] > 0x1p-53) {
         for (bk_ctx *c : g->ctx) c->force_exact = 1;
         int st = BK_OK;
         for (int r = 0; r < G && st == BK_OK; ++r) {
