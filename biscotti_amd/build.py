@@ -52,8 +52,16 @@ def build(force=False, verbose=True, extra=(), out=LIB, jobs=None):
     if not force and out == LIB and not needs_build():
         return LIB
     import concurrent.futures as cf
+    import hashlib
+    import shutil
     import tempfile
-    tmp = tempfile.mkdtemp(prefix="bk_build_")
+    # a fixed object directory per (output, flags): the object paths end up in
+    # the linked library, and a random temp name made every build's sha256
+    # differ (the PMC records are matched to the library by that hash)
+    key = hashlib.sha1(("\0".join([out] + list(extra))).encode()).hexdigest()[:12]
+    tmp = os.path.join(tempfile.gettempdir(), "bk_build_" + key)
+    shutil.rmtree(tmp, ignore_errors=True)
+    os.makedirs(tmp)
     cflags = [f for f in FLAGS if f != "-shared"] + list(extra)
     objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]
 
@@ -71,7 +79,6 @@ def build(force=False, verbose=True, extra=(), out=LIB, jobs=None):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
-    import shutil
     shutil.rmtree(tmp, ignore_errors=True)
     return out
 
