@@ -2057,7 +2057,6 @@ static int check_roni(int64_t nv, int64_t d, int64_t ldv, int64_t n, int64_t ld)
     if (ldv < d) return fail(BK_EINVAL, "ldv=%lld < d=%lld", (long long)ldv, (long long)d);
     if (n < 0) return fail(BK_EINVAL, "n=%lld < 0", (long long)n);
     if (n > 0 && ld < d) return fail(BK_EINVAL, "ld=%lld < d=%lld", (long long)ld, (long long)d);
-    if (d > 1024) return fail(BK_ENOTSUP, "RONI d=%lld exceeds 1024", (long long)d);
     if (n > 65534) return fail(BK_ENOTSUP, "RONI n=%lld exceeds 65534", (long long)n);
     return BK_OK;
 }
@@ -2073,9 +2072,11 @@ int bk_roni_device(bk_ctx *c, const double *d_Xv, int64_t nv, int64_t d, int64_t
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
+    CHK(ensure(c->rmc_ws, roni_ws(n, d)));
     unsigned int *cnt = (unsigned int *)c->roni_cnt.p;
     return timed(c, BK_K_RONI, [&] {
-        return launch_roni(d_Xv, nv, d, ldv, d_yv, d_ww, d_deltas, n, ld, cnt, d_scores, c->stream);
+        return launch_roni(d_Xv, nv, d, ldv, d_yv, d_ww, d_deltas, n, ld, (double *)c->rmc_ws.p, cnt,
+                           d_scores, c->stream);
     });
 }
 
@@ -2117,6 +2118,7 @@ int bk_roni(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_
     CHK(ensure(c->roni_d, (size_t)n * d * sizeof(double)));
     CHK(ensure(c->roni_s, (size_t)n * sizeof(double)));
     CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
+    CHK(ensure(c->rmc_ws, roni_ws(n, d)));
     double *dw = (double *)c->roni_w.p, *dd = (double *)c->roni_d.p, *ds = (double *)c->roni_s.p;
     CHK(timed(c, BK_K_H2D, [&] {
         hipError_t e = hipMemcpyAsync(dw, ww, (size_t)d * sizeof(double), hipMemcpyHostToDevice,
@@ -2129,7 +2131,7 @@ int bk_roni(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_
     }));
     CHK(timed(c, BK_K_RONI, [&] {
         return launch_roni((const double *)c->roni_X.p, c->roni_nv, d, d,
-                           (const double *)c->roni_y.p, dw, dd, n, d,
+                           (const double *)c->roni_y.p, dw, dd, n, d, (double *)c->rmc_ws.p,
                            (unsigned int *)c->roni_cnt.p, ds, c->stream);
     }));
     CHK(timed(c, BK_K_D2H, [&] {
@@ -2166,7 +2168,7 @@ int bk_roni_softmax_device(bk_ctx *c, const float *d_Xv, int64_t nv, int64_t d_i
     if (n == 0) return BK_OK;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
-    CHK(ensure(c->rmc_ws, roni_softmax_ws(n, d_in)));
+    CHK(ensure(c->rmc_ws, roni_softmax_ws(n, d_in, nv, (int)n_classes)));
     CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
     return timed(c, BK_K_RONI, [&] {
         return launch_roni_softmax(d_Xv, nv, d_in, ldv, d_yv, (int)n_classes, d_ww, d_deltas, n,
@@ -2212,7 +2214,7 @@ int bk_roni_softmax(bk_ctx *c, const double *ww, const double *deltas, int64_t n
     CHK(ensure(c->roni_w, (size_t)d * sizeof(double)));
     CHK(ensure(c->roni_d, (size_t)n * d * sizeof(double)));
     CHK(ensure(c->roni_s, (size_t)n * sizeof(double)));
-    CHK(ensure(c->rmc_ws, roni_softmax_ws(n, din)));
+    CHK(ensure(c->rmc_ws, roni_softmax_ws(n, din, c->rmc_nv, (int)C)));
     CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
     double *dw = (double *)c->roni_w.p, *dd = (double *)c->roni_d.p, *ds = (double *)c->roni_s.p;
     CHK(timed(c, BK_K_H2D, [&] {

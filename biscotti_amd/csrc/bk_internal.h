@@ -128,11 +128,13 @@ hipError_t launch_noise(const double *delta, int64_t ld, int64_t n, int64_t d, c
                         hipStream_t st);
 hipError_t configure_aggregate_kernels();
 // bk_roni.hip
+// K7: ws = roni_ws(n, d) bytes (the models' weights, k-major)
+size_t roni_ws(int64_t n, int64_t d);
 hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, const double *yv,
                        const double *ww, const double *deltas, int64_t n, int64_t ld,
-                       unsigned int *cnt, double *scores, hipStream_t st);
-// the torch-path (softmax model) RONI, K8: ws = roni_softmax_ws(n, din) bytes
-size_t roni_softmax_ws(int64_t n, int64_t din);
+                       double *ws, unsigned int *cnt, double *scores, hipStream_t st);
+// the torch-path (softmax model) RONI, K8: ws = roni_softmax_ws(n, din, nv, C) bytes
+size_t roni_softmax_ws(int64_t n, int64_t din, int64_t nv, int C);
 hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
                                const int32_t *yv, int C, const double *ww, const double *deltas,
                                int64_t n, int64_t ld, double *ws, unsigned int *good,

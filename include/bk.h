@@ -322,8 +322,9 @@ int bk_multikrum_noised(bk_ctx *ctx, const double *delta, int64_t ld, const doub
  * with numpy's sign (0 -> 0, NaN -> NaN, which never equals a label).  Xv is
  * nv x d (row stride ldv), yv the nv labels as doubles (creditcard: -1 / +1,
  * utils.py:96-97), ww d weights, deltas n x d (row stride ld).  The Go verifier
- * rejects an update whose score exceeds 0.02 (main.go:213-226).  d <= 1024
- * (16 models x d fp64 in LDS; creditcard d = 25), n <= 65534. */
+ * rejects an update whose score exceeds 0.02 (main.go:213-226).  Any d
+ * (creditcard d = 25), n <= 65534.  Each dot is the fp64 FMA chain over k
+ * ascending (on the fp64 MFMA, which rounds exactly so). */
 int bk_roni_device(bk_ctx *ctx, const double *d_Xv, int64_t nv, int64_t d, int64_t ldv,
                    const double *d_yv, const double *d_ww, const double *d_deltas, int64_t n,
                    int64_t ld, double *d_scores);

@@ -49,7 +49,9 @@ def test_roni_goldens_host_validator(engine, name):
 
 
 @pytest.mark.parametrize("nv,d,n", [(200_000, 25, 16), (4096, 25, 512), (3000, 785, 33),
-                                    (1, 1, 1), (1025, 1024, 2), (777, 25, 15), (778, 25, 16)])
+                                    (1, 1, 1), (1025, 1024, 2), (777, 25, 15), (778, 25, 16),
+                                    # r3b: no cap on d (the MFMA form keeps no model in LDS)
+                                    (2000, 7850, 9), (513, 3001, 130)])
 def test_roni_vs_oracle(engine, oracle, nv, d, n):
     rng = np.random.default_rng(nv + d + n)
     Xv = np.hstack([np.ones((nv, 1)), rng.standard_normal((nv, d - 1))]) if d > 1 else \
