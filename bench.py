@@ -412,18 +412,17 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
         t = eng.timing_read().get("k_roni" if name.startswith("k_roni") else name)
         eng.timing_enable(False)
         ms = t["avg_ms"]
-        if name == "k_roni_softmax":  # fp64 VALU FMAs: nv x (n+1) x C x d_in
-            fl = 2.0 * nvm * (nrm + 1) * cm * dinm
+        if name.startswith("k_roni"):  # fp64 MFMA GEMMs (r3b): algorithmic flops
+            if name == "k_roni_softmax":  # nv x (n+1) x C x d_in
+                fl, nu = 2.0 * nvm * (nrm + 1) * cm * dinm, nrm
+            else:  # nv x (n+1) x d
+                fl, nu = 2.0 * nv * (nr + 1) * dr, nr
             res[name] = {"what": what, "ms": round(ms, 4),
-                         "updates_per_s": round(nrm / (ms * 1e-3), 1),
+                         "updates_per_s": round(nu / (ms * 1e-3), 1),
                          "fp64_tflops": round(fl / (ms * 1e-3) / 1e12, 3),
-                         "roofline": {"bound": "valu", "peak": 78.6, "unit": "TFLOP/s",
-                                      "frac": round(fl / (ms * 1e-3) / 1e12 / 78.6, 4)}}
-            continue
-        if nbytes is None:  # RONI: latency / L2-bound, reported as a rate
-            res[name] = {"what": what, "ms": round(ms, 4),
-                         "updates_per_s": round(nr / (ms * 1e-3), 1),
-                         "validation_dots_per_s": round(nv * (nr + 1) / (ms * 1e-3), 1)}
+                         "roofline": {"bound": "mfma", "peak": 78.6, "unit": "TFLOP/s",
+                                      "frac": round(fl / (ms * 1e-3) / 1e12 / 78.6, 4),
+                                      "note": "whole launch (weights prep, GEMM, count, score)"}}
             continue
         gbs = nbytes / (ms * 1e-3) / 1e9
         res[name] = {"what": what, "ms": round(ms, 4), "bytes": nbytes, "GB_per_s": round(gbs, 1),

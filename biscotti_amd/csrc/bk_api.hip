@@ -2058,6 +2058,7 @@ static int check_roni(int64_t nv, int64_t d, int64_t ldv, int64_t n, int64_t ld)
     if (n < 0) return fail(BK_EINVAL, "n=%lld < 0", (long long)n);
     if (n > 0 && ld < d) return fail(BK_EINVAL, "ld=%lld < d=%lld", (long long)ld, (long long)d);
     if (n > 65534) return fail(BK_ENOTSUP, "RONI n=%lld exceeds 65534", (long long)n);
+    if (d > ((int64_t)1 << 21)) return fail(BK_ENOTSUP, "RONI d=%lld exceeds 2^21", (long long)d);
     return BK_OK;
 }
 
@@ -2155,6 +2156,7 @@ static int check_roni_softmax(int64_t nv, int64_t din, int64_t ldv, int64_t C, i
                     (long long)(C * (din + 1)));
     if (n > 262139) return fail(BK_ENOTSUP, "RONI n=%lld exceeds 262139", (long long)n);
     if (nv > ((int64_t)1 << 31)) return fail(BK_ENOTSUP, "RONI nv=%lld too large", (long long)nv);
+    if (din > ((int64_t)1 << 21)) return fail(BK_ENOTSUP, "RONI d_in=%lld exceeds 2^21", (long long)din);
     return BK_OK;
 }
 

@@ -244,72 +244,112 @@ __global__ void k_roni_mc_score(const unsigned int *__restrict__ good, int64_t n
 }
 
 // ---------------------------------------------------------------------------
-// K8 on the matrix pipe (r3b).  The n + 1 models' logits are one GEMM:
-// L[s][j C + c] = sum_k x[s][k] W_j[c][k], M = nv samples, N = (n + 1) C
-// model-class columns, K = d_in.  v_mfma_f64_16x16x4_f64 rounds like four
-// fp64 FMAs in k order (tools/probe_mfma_order.hip), so a chain of
-// them over k ascending from +0.0 is the same fp64 sum, bit for bit, as K8's
-// per-lane FMA chain -- and as the oracle's.
+// K8 on the matrix pipe (r3b).  The n + 1 models' logits are one GEMM,
+// sum_k x[s][k] W_j[c][k] for M = nv samples, N = (n + 1) C model-class
+// columns, K = d_in.  v_mfma_f64_16x16x4_f64 rounds like four fp64 FMAs in k
+// order (tools/probe_mfma_order.hip), so a chain of them over k
+// ascending from +0.0 is the same fp64 sum, bit for bit, as K8's per-lane FMA
+// chain -- and as the oracle's.
 //
-//   K8a' k_roni_mm_prep   Wt[k][j C + c] = fp32(ww + delta_j) widened, the
-//                         columns padded to RMM_NT, rows to a multiple of 8;
-//                         bt[col] the biases
-//   K8b' k_roni_mm_logits grid (64-sample tiles, 128-column tiles), 4 waves,
-//                         each 32 samples x 64 columns (2 x 4 MFMA blocks):
-//                         the tile's samples staged 64 features at a time in
-//                         LDS ([k][sample], row stride 80 floats: the A
-//                         fragment reads hit distinct banks), the B fragments
-//                         from L2 (every sample tile reads the same Wt);
-//                         logit = fp32(acc + b) stored to L
-//   K8c' k_roni_mm_count  wave w: model 4 y + w, lane l: sample 64 x + l: the
-//                         argmax of the C logits, one ballot count per wave
-// Bound: fp64 MFMA (nv x (n+1) C x d_in MACs); L is nv x ldL fp32 (24.6 MB at
-// the mnist bench shape), written and read once.
-constexpr int RMM_MT = 64, RMM_NT = 128, RMM_KC = 64, RMM_XS = 80;
+// Columns: a 128-column tile holds P = 128 / C whole models (tile y: models
+// P y .. P y + P - 1, column (j - P y) C + c), the rest zero padding (at most
+// C - 1 columns: 8 of 128 for mnist's 10 classes), so the argmax never crosses
+// a tile.  K7 uses the same layout with C = 1.
+//
+//   K8a' k_roni_mm_prep   Wt[k][col] = fp32(ww + delta_j) widened (K7: the
+//                         fp64 sum), rows padded to a multiple of 32; bt[col]
+//                         the biases.  32 k x 64 columns per workgroup through
+//                         LDS: reads run along k (the flat weights' order),
+//                         writes along the columns
+//   K8b' k_roni_logits    the logits GEMM with the argmax and the count fused
+//                         into its epilogue (below)
+// Bound: fp64 MFMA (nv x (n+1) C x d_in MACs).
+constexpr int RMM_NT = 128;  // columns per tile (= RG_NT below)
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 static inline int64_t rmm_ldl(int64_t n, int C) {
-    return ((n + 1) * C + RMM_NT - 1) / RMM_NT * RMM_NT;
+    const int64_t P = RMM_NT / C;
+    return (n + 1 + P - 1) / P * RMM_NT;
 }
-static inline int64_t rmm_rows(int64_t din) { return (din + 7) / 8 * 8; }
+static inline int64_t rmm_rows(int64_t din) { return (din + 31) / 32 * 32; }  // whole K7 chunks
 
-// softmax (K8): fp32(ww + delta_j) widened, plus the bias row `rows`;
-// logistic (K7): ww + delta_j in fp64 (numpy's add), no bias
+// softmax (K8): fp32(ww + delta_j) widened, plus the biases; logistic (K7):
+// ww + delta_j in fp64 (numpy's add), no bias.  Grid (ldl / 64, rows / 32).
 template <bool SOFTMAX>
 __global__ __launch_bounds__(256) void k_roni_mm_prep(const double *__restrict__ ww,
                                                       const double *__restrict__ deltas, int64_t ld,
-                                                      int64_t din, int C, int64_t nmod, int64_t rows,
-                                                      int64_t ldl, double *__restrict__ Wt,
+                                                      int64_t din, int C, int64_t nmod, int64_t ldl,
+                                                      int64_t rows, double *__restrict__ Wt,
                                                       double *__restrict__ bt) {
-    for (int64_t k = blockIdx.y; k < rows + (SOFTMAX ? 1 : 0); k += gridDim.y)
-        for (int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x; col < ldl;
-             col += (int64_t)gridDim.x * 256) {
-            const int64_t j = col / C;
-            const int c = (int)(col - j * C);
-            const bool bias = SOFTMAX && k == rows;
+    __shared__ double tile[32][65];
+    const int tid = threadIdx.x;
+    const int P = RMM_NT / C;
+    const int64_t col0 = (int64_t)blockIdx.x * 64, k0 = (int64_t)blockIdx.y * 32;
+    {  // read: thread t -> column t >> 2, features (t & 3) * 8 .. + 7 (contiguous in the source)
+        const int lc = tid >> 2, kk = (tid & 3) * 8;
+        const int64_t col = col0 + lc;
+        const int64_t y = col / RMM_NT;
+        const int w = (int)(col - y * RMM_NT), p = w / C, c = w - p * C;
+        const int64_t j = y * P + p;
+        const bool live = p < P && j < nmod;
+        const double *src0 = ww + (int64_t)c * din;
+        const double *src1 = deltas + (j > 0 ? (j - 1) * ld : 0) + (int64_t)c * din;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = k0 + kk + u;
             double v = 0.0;  // padding: zero weights (x * 0 adds +0 to a chain that is never -0)
-            if (j < nmod && (bias || k < din)) {
-                const int64_t idx = bias ? (int64_t)C * din + c : (int64_t)c * din + k;
-                v = j == 0 ? ww[idx] : ww[idx] + deltas[(j - 1) * ld + idx];
+            if (live && k < din) {
+                v = j == 0 ? src0[k] : src0[k] + src1[k];
                 if (SOFTMAX) v = (double)(float)v;
             }
-            if (bias)
-                bt[col] = v;
-            else
-                Wt[k * ldl + col] = v;
+            tile[kk + u][lc] = v;
         }
+        if (SOFTMAX && blockIdx.y == 0 && (tid & 3) == 0) {
+            double v = 0.0;
+            if (live) {
+                const int64_t idx = (int64_t)C * din + c;
+                v = (double)(float)(j == 0 ? ww[idx] : ww[idx] + deltas[(j - 1) * ld + idx]);
+            }
+            bt[col] = v;
+        }
+    }
+    __syncthreads();
+    // write: 64 consecutive columns of 4 rows per pass
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int kk = u * 4 + (tid >> 6), lc = tid & 63;
+        if (k0 + kk < rows) Wt[(k0 + kk) * ldl + col0 + lc] = tile[kk][lc];
+    }
 }
 
-__global__ __launch_bounds__(256) void k_roni_mm_logits(const float *__restrict__ Xv, int64_t nv,
-                                                        int64_t din, int64_t ldv,
-                                                        const double *__restrict__ Wt,
-                                                        const double *__restrict__ bt, int64_t ldl,
-                                                        int nx, int xcd_cols, float *__restrict__ L) {
-    __shared__ float xs[RMM_KC][RMM_XS];
+// K8b' k_roni_logits: 64-sample x 128-column tiles, 4 waves of 32 samples x
+// 64 columns (2 x 4 MFMA blocks), three waves per SIMD (752 tiles at the
+// mnist bench shape fill the chip's 768 workgroup slots in one round; a
+// split of k would break the FMA chain's order, so the tiles carry all of k).
+// The samples go through LDS in chunks of 64 features ([sample][k], row
+// stride 68 floats: the A fragment's 16 rows x 4 k and a staging write's 64
+// lanes along k hit distinct banks; the next chunk's loads are in flight
+// under this chunk's MFMAs); the B fragments come from L2 one k-step ahead,
+// into alternating register sets.  Epilogue: logit = fp32(acc + b) into an
+// LDS tile, then wave w takes models w, w + 4, ... of the tile, lane l sample
+// l: np.argmax over the C logits, one ballot count and one atomic per model
+// and workgroup.
+constexpr int RG_MT = 64, RG_NT = 128, RG_LT = RG_NT + 1;
+constexpr int RL_KC = 64, RL_XS = 68;
+
+__global__ __launch_bounds__(256) void k_roni_logits(const float *__restrict__ Xv, int64_t nv,
+                                                     int64_t din, int64_t ldv,
+                                                     const int32_t *__restrict__ yv, int C,
+                                                     const double *__restrict__ Wt,
+                                                     const double *__restrict__ bt, int64_t ldl,
+                                                     int64_t nmod, int nx, int xcd_cols,
+                                                     unsigned int *__restrict__ good) {
+    __shared__ float xs[RG_MT][RL_XS];
+    __shared__ float lt[RG_MT][RG_LT];
     const int tid = threadIdx.x, l = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave & 1, wn = wave >> 1;
-    // tile (x, y): with xcd_cols, column tile y lives on XCD y mod 8 (blocks
+    // tile (x, y): with xcd_cols, column tile y lives on XCD y mod 8 (block
     // numbers = y mod 8), so an XCD's L2 holds only its eighth of Wt
     const int blk = blockIdx.x;
     int tx, ty;
@@ -321,36 +361,37 @@ __global__ __launch_bounds__(256) void k_roni_mm_logits(const float *__restrict_
         tx = blk % nx;
         ty = blk / nx;
     }
-    const int64_t s0 = (int64_t)tx * RMM_MT;
-    const int64_t c0 = (int64_t)ty * RMM_NT + 64 * wn;
+    const int64_t s0 = (int64_t)tx * RG_MT;
+    const int64_t cb = (int64_t)ty * RG_NT, c0 = cb + 64 * wn;
     d4 acc[2][4];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) acc[a][bb] = d4{0.0, 0.0, 0.0, 0.0};
-    // staging: thread t moves features (t & 3) * 16 .. + 15 of sample t >> 2;
-    // the next chunk's loads are in flight during this chunk's MFMAs
-    const int ts = tid >> 2, tk = (tid & 3) * 16;
-    const int64_t srow = s0 + ts < nv ? s0 + ts : nv - 1;
-    const float *xrow = Xv + srow * ldv;
+    // staging: thread t moves feature t & 63 of samples (t >> 6) + 4 u
+    const int xk = tid & 63, xsr = tid >> 6;
     const double *wcol = Wt + c0 + (l & 15) + (int64_t)(l >> 4) * ldl;
     const int arow = 32 * wm + (l & 15), ak = l >> 4;
     float xv[16];  // clamped addresses, every load in flight
+    auto load_x = [&](int64_t k0) {
+        int64_t k = k0 + xk;
+        k = k < din ? k : din - 1;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) xv[u] = xrow[tk + u < din ? tk + u : din - 1];
-    for (int64_t k0 = 0; k0 < din; k0 += RMM_KC) {
-        __syncthreads();  // the previous chunk has been consumed
-#pragma unroll
-        for (int u = 0; u < 16; ++u) xs[tk + u][ts] = k0 + tk + u < din ? xv[u] : 0.0f;
-        __syncthreads();
-        if (k0 + RMM_KC < din) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int64_t k = k0 + RMM_KC + tk + u;
-                xv[u] = xrow[k < din ? k : din - 1];
-            }
+        for (int u = 0; u < 16; ++u) {
+            int64_t s = s0 + xsr + 4 * u;
+            s = s < nv ? s : nv - 1;
+            xv[u] = Xv[s * ldv + k];
         }
-        const int kn = (int)(din - k0 < RMM_KC ? din - k0 : RMM_KC);
+    };
+    load_x(0);
+    for (int64_t k0 = 0; k0 < din; k0 += RL_KC) {
+        __syncthreads();  // the previous chunk has been consumed
+        const bool kin = k0 + xk < din;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xs[xsr + 4 * u][xk] = kin ? xv[u] : 0.0f;
+        __syncthreads();
+        if (k0 + RL_KC < din) load_x(k0 + RL_KC);
+        const int kn = (int)(din - k0 < RL_KC ? din - k0 : RL_KC);
         // k-steps in pairs (rows past d_in are zero in LDS and in Wt), the B
         // fragments of the next step loaded before this step's MFMAs, into the
         // other register set: their L2 latency runs under the MFMAs
@@ -364,8 +405,8 @@ __global__ __launch_bounds__(256) void k_roni_mm_logits(const float *__restrict_
             const int64_t o2 = (int64_t)(st + 2 < steps ? st + 2 : st + 1) * 4 * ldl;
 #pragma unroll
             for (int b = 0; b < 4; ++b) b1[b] = wk[o1 + 16 * b];
-            double a0 = (double)xs[4 * st + ak][arow];
-            double a1 = (double)xs[4 * st + ak][arow + 16];
+            double a0 = (double)xs[arow][4 * st + ak];
+            double a1 = (double)xs[arow + 16][4 * st + ak];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 acc[0][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[b], acc[0][b], 0, 0, 0);
@@ -373,8 +414,8 @@ __global__ __launch_bounds__(256) void k_roni_mm_logits(const float *__restrict_
             }
 #pragma unroll
             for (int b = 0; b < 4; ++b) b0[b] = wk[o2 + 16 * b];
-            a0 = (double)xs[4 * st + 4 + ak][arow];
-            a1 = (double)xs[4 * st + 4 + ak][arow + 16];
+            a0 = (double)xs[arow][4 * st + 4 + ak];
+            a1 = (double)xs[arow + 16][4 * st + 4 + ak];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 acc[0][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1[b], acc[0][b], 0, 0, 0);
@@ -385,47 +426,170 @@ __global__ __launch_bounds__(256) void k_roni_mm_logits(const float *__restrict_
     // D reg r of lane l: sample row (l >> 4) + 4 r of the block, column l & 15
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-        const int64_t col = c0 + 16 * b + (l & 15);
-        const double bias = bt[col];
+        const int lc = 64 * wn + 16 * b + (l & 15);
+        const double bias = bt[cb + lc];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                lt[32 * wm + 16 * a + (l >> 4) + 4 * r][lc] = (float)(acc[a][b][r] + bias);
+    }
+    __syncthreads();
+    // np.argmax: the first maximum, a NaN wins at its first place
+    const int P = RG_NT / C;
+    const int64_t s = s0 + l;
+    const int ysl = yv[s < nv ? s : nv - 1];
+    for (int p = wave; p < P; p += 4) {
+        const int64_t j = (int64_t)ty * P + p;
+        if (j >= nmod) break;  // wave-uniform
+        const float *lg = &lt[l][p * C];
+        int best = 0;
+        float bl = lg[0];
+        for (int c = 1; c < C; ++c) {
+            const float v = lg[c];
+            if (!(bl != bl) && (v != v || v > bl)) {
+                best = c;
+                bl = v;
+            }
+        }
+        const unsigned int ok = (unsigned int)__popcll(__ballot(s < nv && best == ysl));
+        if (l == 0 && ok) atomicAdd(&good[j], ok);
+    }
+}
+
+// K7' k_roni_sign: the logistic verifier's GEMM (fp64 samples, one model per
+// column) with the sign test fused into its epilogue.  Same 64 x 128 tiles
+// and waves; both operands through LDS in chunks of 32 k ([sample][k] row
+// stride 34 doubles, [k][column] row stride 144 doubles: every fragment read
+// and staging write on distinct banks), the next chunk's loads in registers
+// under this chunk's MFMAs (and the tile's labels with its first chunk).  A
+// workgroup walks tiles_per_wg (8) sample tiles; with d <= 32 (creditcard:
+// 25) the weights are staged once.  Counts stay in
+// registers; two lane butterflies and one atomic per model and wave at the end.
+constexpr int RS_KC = 32, RS_XS = 34, RS_BS = 144;
+
+__global__ __launch_bounds__(256) void k_roni_sign(const double *__restrict__ Xv, int64_t nv,
+                                                   int64_t din, int64_t ldv,
+                                                   const double *__restrict__ yv,
+                                                   const double *__restrict__ Wt, int64_t ldl,
+                                                   int64_t nmod, int nx, int tiles_per_wg,
+                                                   unsigned int *__restrict__ cnt) {
+    __shared__ double xs[RG_MT][RS_XS];
+    __shared__ double bs[RS_KC][RS_BS];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    const int tx = blockIdx.x % nx, ty = blockIdx.x / nx;
+    const int64_t tiles = (nv + RG_MT - 1) / RG_MT;
+    const int64_t t0 = (int64_t)tx * tiles_per_wg;
+    const int nt = (int)(tiles - t0 < tiles_per_wg ? tiles - t0 : tiles_per_wg);
+    const int nch = (int)((din + RS_KC - 1) / RS_KC);
+    const int ni = nt * nch;
+    const bool restage_b = nch > 1;
+    const int64_t cb = (int64_t)ty * RG_NT;  // the tile's first column
+    // staging maps (global loads coalesced, LDS writes conflict-free): sample
+    // (t >> 5) + 8 u, feature t & 31; weights row 2 u + (t >> 7), column t & 127
+    const int xs_s = tid >> 5, xs_k = tid & 31;
+    const int bs_k = tid >> 7, bs_c = tid & 127;
+    double xv[8], bv[16], yn[8], yc[8];
+    // y of this lane's 8 epilogue rows (a, r), loaded with the tile's first chunk
+    auto load_y = [&](int tt) {
+        const int64_t s0 = (t0 + tt) * RG_MT + 32 * wm + (l >> 4);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t s = s0 + 16 * a + 4 * r;
+                yn[4 * a + r] = yv[s < nv ? s : nv - 1];
+            }
+    };
+    auto prefetch = [&](int it, bool with_b) {
+        const int tt = it / nch, ch = it - tt * nch;
+        if (ch == 0) load_y(tt);
+        int64_t k = (int64_t)ch * RS_KC + xs_k;
+        k = k < din ? k : din - 1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            int64_t s = (t0 + tt) * RG_MT + xs_s + 8 * u;
+            s = s < nv ? s : nv - 1;
+            xv[u] = Xv[s * ldv + k];
+        }
+        if (with_b) {
+            const double *br = Wt + ((int64_t)ch * RS_KC + bs_k) * ldl + cb + bs_c;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) bv[u] = br[2 * u * ldl];
+        }
+    };
+    d4 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) acc[a][bb] = d4{0.0, 0.0, 0.0, 0.0};
+    unsigned int mis[4] = {0, 0, 0, 0};
+    const int arow = 32 * wm + (l & 15), ak = l >> 4;
+    const int bcol = 64 * wn + (l & 15);
+    prefetch(0, true);
+    for (int it = 0; it < ni; ++it) {
+        const int tt = it / nch, ch = it - tt * nch;
+        __syncthreads();  // the previous chunk has been consumed
+        const bool kin = (int64_t)ch * RS_KC + xs_k < din;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) xs[xs_s + 8 * u][xs_k] = kin ? xv[u] : 0.0;
+        if (restage_b || it == 0) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) bs[bs_k + 2 * u][bs_c] = bv[u];
+        }
+        __syncthreads();
+        if (ch == 0) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) yc[q] = yn[q];
+        }
+        if (it + 1 < ni) prefetch(it + 1, restage_b);
+        const int64_t kr = din - (int64_t)ch * RS_KC;
+        const int steps = ((int)(kr < RS_KC ? kr : RS_KC) + 3) >> 2;  // rows past d are zero
+        for (int st = 0; st < steps; ++st) {
+            const double a0 = xs[arow][4 * st + ak], a1 = xs[arow + 16][4 * st + ak];
+            double bf[4];
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) bf[bb] = bs[4 * st + ak][bcol + 16 * bb];
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) {
+                acc[0][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bf[bb], acc[0][bb], 0, 0, 0);
+                acc[1][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bf[bb], acc[1][bb], 0, 0, 0);
+            }
+        }
+        if (ch != nch - 1) continue;
+        // D reg r of lane l: sample row (l >> 4) + 4 r of the block, model column l & 15
+        const int64_t s0 = (t0 + tt) * RG_MT;
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t s = s0 + 32 * wm + 16 * a + (l >> 4) + 4 * r;
-                if (s < nv) L[s * ldl + col] = (float)(acc[a][b][r] + bias);
+                const double y = yc[4 * a + r];
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    const double v = acc[a][bb][r];  // np.sign: 0 -> 0, NaN -> NaN
+                    const double yh = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : (v == 0.0 ? 0.0 : v));
+                    mis[bb] += (s < nv && !(yh == y)) ? 1u : 0u;
+                    acc[a][bb][r] = 0.0;
+                }
             }
     }
-}
-
-__global__ __launch_bounds__(256) void k_roni_mm_count(const float *__restrict__ L, int64_t nv,
-                                                       int64_t ldl, const int32_t *__restrict__ yv,
-                                                       int C, int64_t nmod,
-                                                       unsigned int *__restrict__ good) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int64_t j = (int64_t)blockIdx.y * 4 + (tid >> 6);
-    const int64_t s = (int64_t)blockIdx.x * 64 + lane;
-    if (j >= nmod) return;  // wave-uniform
-    const int64_t sr = s < nv ? s : nv - 1;
-    const float *lg = L + sr * ldl + j * C;
-    // np.argmax: the first maximum, a NaN wins at its first place
-    int best = 0;
-    float bl = lg[0];
-    for (int c = 1; c < C; ++c) {
-        const float v = lg[c];
-        if (!(bl != bl) && (v != v || v > bl)) {
-            best = c;
-            bl = v;
-        }
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+        unsigned int tot = mis[bb];
+        tot += __shfl_xor(tot, 16);
+        tot += __shfl_xor(tot, 32);
+        const int64_t j = cb + 64 * wn + 16 * bb + l;
+        if (l < 16 && tot && j < nmod) atomicAdd(&cnt[j], tot);
     }
-    const bool ok = s < nv && best == yv[sr];
-    const unsigned int cnt = (unsigned int)__popcll(__ballot(ok));
-    if (lane == 0 && cnt) atomicAdd(&good[j], cnt);
 }
 
 size_t roni_softmax_ws(int64_t n, int64_t din, int64_t nv, int C) {
+    (void)nv;
     const int64_t ldl = rmm_ldl(n, C);
-    const size_t mm = (size_t)(rmm_rows(din) + 1) * ldl * sizeof(double) +
-                      (size_t)nv * ldl * sizeof(float);
+    const size_t mm = (size_t)(rmm_rows(din) + 1) * ldl * sizeof(double);
     const size_t mc = (size_t)(n + 1) * ((size_t)din * RMC_CP + RMC_CP) * sizeof(double);
     return mm > mc ? mm : mc;
 }
@@ -436,20 +600,14 @@ static hipError_t launch_roni_softmax_mm(const float *Xv, int64_t nv, int64_t di
                                          unsigned int *good, double *scores, hipStream_t st) {
     const int64_t nmod = n + 1, ldl = rmm_ldl(n, C), rows = rmm_rows(din);
     double *Wt = ws, *bt = ws + rows * ldl;
-    float *L = (float *)(bt + ldl);
     hipError_t e = hipMemsetAsync(good, 0, (size_t)nmod * sizeof(unsigned int), st);
     if (e != hipSuccess) return e;
-    const unsigned gx = (unsigned)((ldl + 255) / 256 < 64 ? (ldl + 255) / 256 : 64);
-    const unsigned gy = (unsigned)(rows + 1 < 8192 ? rows + 1 : 8192);
-    hipLaunchKernelGGL(k_roni_mm_prep<true>, dim3(gx, gy), dim3(256), 0, st, ww, deltas, ld, din, C, nmod,
-                       rows, ldl, Wt, bt);
+    hipLaunchKernelGGL(k_roni_mm_prep<true>, dim3((unsigned)(ldl / 64), (unsigned)((rows + 31) / 32)),
+                       dim3(256), 0, st, ww, deltas, ld, din, C, nmod, ldl, rows, Wt, bt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const int nx = (int)((nv + RMM_MT - 1) / RMM_MT), ny = (int)(ldl / RMM_NT);
-    hipLaunchKernelGGL(k_roni_mm_logits, dim3((unsigned)(nx * ny)), dim3(256), 0, st, Xv, nv, din,
-                       ldv, Wt, bt, ldl, nx, ny % 8 == 0 ? 1 : 0, L);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_roni_mm_count, dim3((unsigned)((nv + 63) / 64), (unsigned)((nmod + 3) / 4)),
-                       dim3(256), 0, st, L, nv, ldl, yv, C, nmod, good);
+    const int nx = (int)((nv + RG_MT - 1) / RG_MT), ny = (int)(ldl / RG_NT);
+    hipLaunchKernelGGL(k_roni_logits, dim3((unsigned)(nx * ny)), dim3(256), 0, st, Xv, nv, din, ldv,
+                       yv, C, Wt, bt, ldl, nmod, nx, ny % 8 == 0 ? 1 : 0, good);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_roni_mc_score, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, good,
                        n, nv, scores);
@@ -487,104 +645,10 @@ hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t
 
 // ---------------------------------------------------------------------------
 // K7 on the matrix pipe (r3b): S[s][j] = x_s . w_j as one GEMM (M = nv
-// samples, N = n + 1 models, K = d), a chain of v_mfma_f64_16x16x4_f64 over k
-// ascending from +0.0 -- the same fp64 FMA chain as K7's VALU kernel and the
-// oracle, bit for bit -- and the sign test fused into the epilogue: each lane
-// counts the mismatches of its column over its rows, two lane butterflies sum
-// a column's 16 lanes, one atomic per model and wave.  A workgroup walks
-// RSG_T sample tiles of 64 (the counts stay in registers), 4 waves of 32
-// samples x 64 models.  The validation rows are staged 32 features at a time
-// in LDS ([k][sample] fp64, row stride 80: the A fragment reads hit distinct
-// banks), the models come from L2.  No cap on d (K7's LDS model held d <= 1024).
-constexpr int RSG_T = 8, RSG_KC = 32, RSG_XS = 80;
-
-__global__ __launch_bounds__(256) void k_roni_mm_sign(const double *__restrict__ Xv, int64_t nv,
-                                                      int64_t d, int64_t ldv,
-                                                      const double *__restrict__ yv,
-                                                      const double *__restrict__ Wt, int64_t ldl,
-                                                      int64_t nmod, unsigned int *__restrict__ cnt) {
-    __shared__ double xs[RSG_KC][RSG_XS];
-    const int tid = threadIdx.x, l = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave & 1, wn = wave >> 1;
-    const int64_t c0 = (int64_t)blockIdx.y * RMM_NT + 64 * wn;
-    const double *wcol = Wt + c0 + (l & 15) + (int64_t)(l >> 4) * ldl;
-    const int arow = 32 * wm + (l & 15), ak = l >> 4;
-    const int ts = tid >> 2, tk = (tid & 3) * 8;  // staging: 8 features of one sample
-    unsigned int mis[4] = {0, 0, 0, 0};
-    for (int t = 0; t < RSG_T; ++t) {
-        const int64_t s0 = ((int64_t)blockIdx.x * RSG_T + t) * 64;
-        if (s0 >= nv) break;  // uniform
-        d4 acc[2][4];
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-        const int64_t srow = s0 + ts < nv ? s0 + ts : nv - 1;
-        const double *xrow = Xv + srow * ldv;
-        for (int64_t k0 = 0; k0 < d; k0 += RSG_KC) {
-            __syncthreads();  // the previous chunk (or tile) has been consumed
-            double xv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int64_t k = k0 + tk + u;
-                xv[u] = xrow[k < d ? k : d - 1];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) xs[tk + u][ts] = k0 + tk + u < d ? xv[u] : 0.0;
-            __syncthreads();
-            const int kn = (int)(d - k0 < RSG_KC ? d - k0 : RSG_KC);
-            const int steps = ((kn + 7) >> 3) << 1;
-            const double *wk = wcol + k0 * ldl;
-            double b0[4], b1[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) b0[b] = wk[16 * b];
-            for (int st = 0; st < steps; st += 2) {
-                const int64_t o1 = (int64_t)(st + 1) * 4 * ldl;
-                const int64_t o2 = (int64_t)(st + 2 < steps ? st + 2 : st + 1) * 4 * ldl;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) b1[b] = wk[o1 + 16 * b];
-                double a0 = xs[4 * st + ak][arow], a1 = xs[4 * st + ak][arow + 16];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    acc[0][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[b], acc[0][b], 0, 0, 0);
-                    acc[1][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0[b], acc[1][b], 0, 0, 0);
-                }
-#pragma unroll
-                for (int b = 0; b < 4; ++b) b0[b] = wk[o2 + 16 * b];
-                a0 = xs[4 * st + 4 + ak][arow];
-                a1 = xs[4 * st + 4 + ak][arow + 16];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    acc[0][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1[b], acc[0][b], 0, 0, 0);
-                    acc[1][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[b], acc[1][b], 0, 0, 0);
-                }
-            }
-        }
-        // D reg r of lane l: sample row (l >> 4) + 4 r of the block, model column l & 15
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t s = s0 + 32 * wm + 16 * a + (l >> 4) + 4 * r;
-                const double y = yv[s < nv ? s : nv - 1];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const double v = acc[a][b][r];  // np.sign: 0 -> 0, NaN -> NaN
-                    const double yh = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : (v == 0.0 ? 0.0 : v));
-                    mis[b] += (s < nv && !(yh == y)) ? 1u : 0u;
-                }
-            }
-    }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        unsigned int tot = mis[b];
-        tot += __shfl_xor(tot, 16);
-        tot += __shfl_xor(tot, 32);
-        const int64_t j = c0 + 16 * b + l;
-        if (l < 16 && tot && j < nmod) atomicAdd(&cnt[j], tot);
-    }
-}
+// samples, N = n + 1 models, K = d) on k_roni_sign: a chain of
+// v_mfma_f64_16x16x4_f64 over k ascending from +0.0 -- the same fp64 FMA
+// chain as K7's VALU kernel and the oracle, bit for bit -- and the sign test
+// fused into the epilogue.  No cap on d (K7's LDS model held d <= 1024).
 
 size_t roni_ws(int64_t n, int64_t d) {
     return (size_t)rmm_rows(d) * ((n + 1 + RMM_NT - 1) / RMM_NT * RMM_NT) * sizeof(double);
@@ -598,14 +662,21 @@ hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, con
     const int64_t nmod = n + 1, ldl = (nmod + RMM_NT - 1) / RMM_NT * RMM_NT, rows = rmm_rows(d);
     hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nmod * sizeof(unsigned int), st);
     if (e != hipSuccess) return e;
-    const unsigned gx = (unsigned)((ldl + 255) / 256 < 64 ? (ldl + 255) / 256 : 64);
-    const unsigned gy = (unsigned)(rows < 8192 ? rows : 8192);
-    hipLaunchKernelGGL(k_roni_mm_prep<false>, dim3(gx, gy), dim3(256), 0, st, ww, deltas, ld, d, 1,
-                       nmod, rows, ldl, ws, (double *)nullptr);
+    hipLaunchKernelGGL(k_roni_mm_prep<false>, dim3((unsigned)(ldl / 64), (unsigned)((rows + 31) / 32)),
+                       dim3(256), 0, st, ww, deltas, ld, d, 1, nmod, ldl, rows, ws, (double *)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const int64_t tiles = (nv + 64 * RSG_T - 1) / (64 * RSG_T);
-    hipLaunchKernelGGL(k_roni_mm_sign, dim3((unsigned)tiles, (unsigned)(ldl / RMM_NT)), dim3(256), 0,
-                       st, Xv, nv, d, ldv, yv, ws, ldl, nmod, cnt);
+    // sample tiles per workgroup (8; BK_RONI_TILES for A/B): more, shorter
+    // workgroups hide each tile's barrier and LDS latency behind the others
+    static const int per_env = [] {
+        const char *e = getenv("BK_RONI_TILES");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 256 ? v : 8;
+    }();
+    const int64_t tiles = (nv + RG_MT - 1) / RG_MT, ny = ldl / RG_NT;
+    const int64_t per = per_env;
+    const int nx = (int)((tiles + per - 1) / per);
+    hipLaunchKernelGGL(k_roni_sign, dim3((unsigned)(nx * ny)), dim3(256), 0, st, Xv, nv, d, ldv, yv,
+                       ws, ldl, nmod, nx, (int)per, cnt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_roni_score, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cnt, n,
                        nv, scores);
