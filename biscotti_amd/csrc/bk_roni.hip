@@ -605,7 +605,9 @@ static hipError_t launch_roni_softmax_mm(const float *Xv, int64_t nv, int64_t di
     hipLaunchKernelGGL(k_roni_mm_prep<true>, dim3((unsigned)(ldl / 64), (unsigned)((rows + 31) / 32)),
                        dim3(256), 0, st, ww, deltas, ld, din, C, nmod, ldl, rows, Wt, bt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const int nx = (int)((nv + RG_MT - 1) / RG_MT), ny = (int)(ldl / RG_NT);
+    const int64_t nx64 = (nv + RG_MT - 1) / RG_MT, ny64 = ldl / RG_NT;
+    if (nx64 * ny64 > 0x7fffffff) return hipErrorInvalidConfiguration;  // grid limit
+    const int nx = (int)nx64, ny = (int)ny64;
     hipLaunchKernelGGL(k_roni_logits, dim3((unsigned)(nx * ny)), dim3(256), 0, st, Xv, nv, din, ldv,
                        yv, C, Wt, bt, ldl, nmod, nx, ny % 8 == 0 ? 1 : 0, good);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -674,7 +676,9 @@ hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, con
     }();
     const int64_t tiles = (nv + RG_MT - 1) / RG_MT, ny = ldl / RG_NT;
     const int64_t per = per_env;
-    const int nx = (int)((tiles + per - 1) / per);
+    const int64_t nx64 = (tiles + per - 1) / per;
+    if (nx64 * ny > 0x7fffffff) return hipErrorInvalidConfiguration;  // grid limit
+    const int nx = (int)nx64;
     hipLaunchKernelGGL(k_roni_sign, dim3((unsigned)(nx * ny)), dim3(256), 0, st, Xv, nv, d, ldv, yv,
                        ws, ldl, nmod, nx, (int)per, cnt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
