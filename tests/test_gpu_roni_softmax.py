@@ -59,6 +59,11 @@ def _device(engine, X, y, C, ww, D):
     (513, 100, 10, 7, {"nan": True}),    # NaN / inf updates: NaN logits win argmax
     (640, 64, 5, 9, {"ties": True}),     # exact logit ties: the first maximum
     (1, 1, 3, 2, {}),
+    # r3b GEMM layout: 8 column tiles (the XCD-mapped grid), C = 16 (8 models
+    # a tile), C = 3 (42 models a tile, 2 padding columns), a ragged d_in
+    (500, 300, 10, 95, {}),
+    (300, 129, 16, 63, {}),
+    (257, 65, 3, 200, {"nan": True}),
 ])
 def test_roni_softmax_vs_oracle(engine, oracle, nv, din, C, n, kw):
     X, y, ww, D = _case(nv, din, C, n, nv + din + C + n, **kw)
