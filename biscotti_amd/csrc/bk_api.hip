@@ -803,7 +803,8 @@ int run_host_outputs(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
 // chunks, no copy stream), the noise added in place by K6 when the verifier
 // noises the batch itself, the kernel, then the outputs and the margin record
 // back, one synchronize.  The device-resident entry's arithmetic, so the same
-// bits.  where == BK_DEVICE skips the copy.
+// bits.  where == BK_DEVICE skips the copy, and so does a pinned batch that
+// k_tiny reads over PCIe itself (below).
 int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, const double *noise,
                    int64_t k, int64_t noise_ld, int64_t n, int64_t d, int64_t f, int64_t *sel_idx,
                    int64_t *m_out, double *scores, double *mean_out, double *noised_out,
@@ -813,7 +814,26 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
     HostDrain drain{c};
     const void *dX = X;
     int64_t dld = ld;
-    if (where != BK_DEVICE) {
+    // a batch k_tiny takes whole (n <= 16, d <= 128: config A, a few KB) is
+    // read by the kernel itself straight from the caller's pinned memory over
+    // PCIe: no H2D copy, whose DMA set-up (~20 us) was most of the call
+    // (BK_TINY_ZERO_COPY=0 copies it as before, for A/B)
+    static const bool tiny_zc = [] {
+        const char *e = getenv("BK_TINY_ZERO_COPY");
+        return !(e && atoi(e) == 0);
+    }();
+    bool zero_copy = false;
+    if (where == BK_HOST_PINNED && k == 0 && !noised_out && tiny_zc && tiny_ok((int)n, d) &&
+        !getenv("BK_SMALL_TRACE")) {
+        void *hp = nullptr;
+        if (hipHostGetDevicePointer(&hp, const_cast<void *>(X), 0) == hipSuccess && hp) {
+            dX = hp;
+            zero_copy = true;
+        } else {
+            (void)hipGetLastError();  // not mapped (pinned by other means): copy it
+        }
+    }
+    if (where != BK_DEVICE && !zero_copy) {
         const int64_t epg = (int64_t)(16 / es);
         dld = (d + epg - 1) / epg * epg;
         CHK(ensure(c->X, (size_t)n * dld * es));

@@ -363,6 +363,11 @@ __global__ __launch_bounds__(256) void k_roni_logits(const float *__restrict__ X
     }
     const int64_t s0 = (int64_t)tx * RG_MT;
     const int64_t cb = (int64_t)ty * RG_NT, c0 = cb + 64 * wn;
+    // a wave whose 64 columns are all padding (the last tile's) skips its
+    // MFMAs: only the staging and the barriers are shared
+    const int P = RG_NT / C;
+    const int64_t live_models = nmod - (int64_t)ty * P < P ? nmod - (int64_t)ty * P : P;
+    const bool live = 64 * wn < live_models * C;
     d4 acc[2][4];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -395,11 +400,11 @@ __global__ __launch_bounds__(256) void k_roni_logits(const float *__restrict__ X
         // k-steps in pairs (rows past d_in are zero in LDS and in Wt), the B
         // fragments of the next step loaded before this step's MFMAs, into the
         // other register set: their L2 latency runs under the MFMAs
-        const int steps = ((kn + 7) >> 3) << 1;
+        const int steps = live ? ((kn + 7) >> 3) << 1 : 0;
         const double *wk = wcol + k0 * ldl;
         double b0[4], b1[4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) b0[b] = wk[16 * b];
+        for (int b = 0; b < 4; ++b) b0[b] = live ? wk[16 * b] : 0.0;
         for (int st = 0; st < steps; st += 2) {
             const int64_t o1 = (int64_t)(st + 1) * 4 * ldl;
             const int64_t o2 = (int64_t)(st + 2 < steps ? st + 2 : st + 1) * 4 * ldl;
@@ -436,7 +441,6 @@ __global__ __launch_bounds__(256) void k_roni_logits(const float *__restrict__ X
     }
     __syncthreads();
     // np.argmax: the first maximum, a NaN wins at its first place
-    const int P = RG_NT / C;
     const int64_t s = s0 + l;
     const int ysl = yv[s < nv ? s : nv - 1];
     for (int p = wave; p < P; p += 4) {

@@ -82,3 +82,43 @@ def test_tiny_is_one_workgroup(engine):
     assert "k_small" in t and "k_gram" not in t, t
     mg = engine.selection_margin()
     assert mg["near_tie"] in (False, True)
+
+
+def test_tiny_host_entry_zero_copy(engine):
+    """r3b: a pinned host batch that k_tiny takes whole is read by the kernel
+    itself over PCIe (no H2D copy: run_host_small).  The same kernel on the same
+    values, so bk_multikrum(BK_HOST_PINNED) must equal the device-resident call
+    byte for byte, odd and padded row strides and fp32 rows included; the
+    evented pass shows the kernel and no copy."""
+    import ctypes
+    from biscotti_amd import _lib
+    L = _lib.lib()
+    for (n, d, f, dt, pad) in SHAPES:
+        tdt = torch.float32 if dt == "f32" else torch.float64
+        bdt = _lib.BK_F32 if dt == "f32" else _lib.BK_F64
+        ld = d + pad
+        X = torch.empty((n, ld), dtype=tdt, device="cuda")
+        engine.synth_fill_ptr(X.data_ptr(), bdt, n, d, ld, 0, d, 1000 + n * 131 + d, f)
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        sc = torch.empty(n, dtype=torch.float64, device="cuda")
+        mn = torch.empty(d, dtype=torch.float64, device="cuda")
+        engine.multikrum_device_ptr(X.data_ptr(), bdt, n, d, ld, f, sel.data_ptr(), sc.data_ptr(),
+                                    mn.data_ptr())
+        engine.synchronize()
+        Xh = torch.empty((n, ld), dtype=tdt, pin_memory=True)
+        Xh.copy_(X)
+        selh = np.empty(n - f, dtype=np.int64)
+        sch = np.empty(n, dtype=np.float64)
+        mnh = np.empty(d, dtype=np.float64)
+        mo = ctypes.c_int64(0)
+        engine.timing_select(["h2d", "k_small"])
+        _lib.check(L.bk_multikrum(engine.ctx, ctypes.c_void_p(Xh.data_ptr()), _lib.BK_HOST_PINNED,
+                                  bdt, n, d, ld, f, selh.ctypes.data, ctypes.addressof(mo),
+                                  sch.ctypes.data, mnh.ctypes.data))
+        kt = engine.timing_read()
+        engine.timing_select([])
+        assert "h2d" not in kt and "k_small" in kt, kt
+        assert mo.value == n - f
+        assert np.array_equal(selh, sel.cpu().numpy()), (n, d, f, dt, pad)
+        assert np.array_equal(sch.view(np.int64), sc.cpu().numpy().view(np.int64))
+        assert np.array_equal(mnh.view(np.int64), mn.cpu().numpy().view(np.int64))
