@@ -90,7 +90,9 @@ int bk_stage_free(bk_ctx *ctx, void *pinned);
  * X on host (BK_HOST / BK_HOST_PINNED: copied H2D) or device (BK_DEVICE).
  * Biscotti's deployed shapes (n <= 128, d <= 32768: the mnist and creditcard
  * verifiers, configs A and B) cross PCIe as ONE copy and run the one-launch
- * path (k_small / k_tiny, see bk_set_small_path).  A larger host batch crosses
+ * path (k_small / k_tiny, see bk_set_small_path); a BK_HOST_PINNED batch that
+ * k_tiny takes whole (n <= 16, d <= 128) is not copied at all: the kernel
+ * reads it over PCIe during the (synchronous) call.  A larger host batch crosses
  * PCIe in column chunks (BK_STAGE_CHUNK_BYTES, default 256 MiB) on a copy
  * stream while the previous chunk's partial Gram runs; the chunk partials are
  * summed in chunk order, so results are deterministic.
