@@ -323,9 +323,10 @@ __global__ __launch_bounds__(256) void k_roni_mm_prep(const double *__restrict__
 }
 
 // K8b' k_roni_logits: 64-sample x 128-column tiles, 4 waves of 32 samples x
-// 64 columns (2 x 4 MFMA blocks), three waves per SIMD (752 tiles at the
-// mnist bench shape fill the chip's 768 workgroup slots in one round; a
-// split of k would break the FMA chain's order, so the tiles carry all of k).
+// 64 columns (2 x 4 MFMA blocks), three waves per SIMD: 768 workgroup slots
+// for the mnist bench shape's 846 tiles (94 sample tiles x 9 column tiles of
+// 12 models; a split of k would break the FMA chain's order, so the tiles
+// carry all of k).
 // The samples go through LDS in chunks of 64 features ([sample][k], row
 // stride 68 floats: the A fragment's 16 rows x 4 k and a staging write's 64
 // lanes along k hit distinct banks; the next chunk's loads are in flight
