@@ -13,6 +13,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     import torch
+    from biscotti_amd import _lib
+    if os.environ.get("LIB"):  # an A/B build (biscotti_amd.build.build(out=...))
+        _lib.LIB_PATH = os.path.abspath(os.environ["LIB"])
     from biscotti_amd._lib import check, lib
     from biscotti_amd.krum import Engine
     eng = Engine(0)
