@@ -320,6 +320,8 @@ def host_entry_variant(eng, dev, name, steps=200, warmup=20, single_calls=7, idl
         torch.cuda.synchronize()
     h2d_ms = (time.perf_counter() - t0) / steps * 1e3
     kname = "k_small" if "k_small" in kt else "k_gram"
+    # k_tiny shares k_small's timing slot (one workgroup for n <= 16, d <= 128)
+    klabel = "k_tiny" if kname == "k_small" and n <= 16 and d <= 128 else kname
     par = golden_check(name, selh.copy(), meanh.copy(), 0, d) or {}
     mg = eng.selection_margin()
     par["margin"] = {"near_tie": mg["near_tie"], "gap": mg["gap"], "err_bound": mg["err_bound"]}
@@ -331,7 +333,7 @@ def host_entry_variant(eng, dev, name, steps=200, warmup=20, single_calls=7, idl
             "single_calls_ms": [round(x, 4) for x in single],
             "h2d_alone_ms": round(h2d_ms, 4),
             "overhead_over_h2d_ms": round(ms - h2d_ms, 4),
-            "kernel": kname, "kernel_avg_ms": round(kt.get(kname, {"avg_ms": float("nan")})["avg_ms"], 4),
+            "kernel": klabel, "kernel_avg_ms": round(kt.get(kname, {"avg_ms": float("nan")})["avg_ms"], 4),
             **({"h2d_evented_ms": round(kt["h2d"]["avg_ms"], 4)} if "h2d" in kt else
                {"input": "read by the kernel from the pinned host batch over PCIe (no H2D copy; "
                          "k_tiny, n <= 16 and d <= 128)"}),
@@ -526,6 +528,10 @@ def small_variant(eng, dev, name="B_mnist", steps=500, warmup=50):
                                         "bound": "hbm" if bytes_alg / PEAK_HBM_GBS > flops / PEAK_TFLOPS["f64"] / 1e3 else "mfma",
                                         "frac": round(t_floor / ms, 4)},
                       "parity": golden_check(name, sel.cpu().numpy(), mean.cpu().numpy(), 0, d)}
+        if res[label]["parity"] is not None:
+            mg = eng.selection_margin()
+            res[label]["parity"]["margin"] = {"near_tie": mg["near_tie"], "gap": mg["gap"],
+                                              "err_bound": mg["err_bound"]}
     eng.set_small_path(True)
     # the one kernel of the one-launch path (k_small, or k_tiny at A), evented
     # on libbk's stream in a pass of its own: its HBM roofline over the
@@ -543,6 +549,8 @@ def small_variant(eng, dev, name="B_mnist", steps=500, warmup=50):
                            "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic,
                            "traffic_source": tsrc, "kernel": "k_tiny" if n <= 16 and d <= 128 else "k_small",
                            "kernel_avg_ms": round(kt["avg_ms"], 5), "bytes_per_launch": bytes_alg}
+        if traffic:
+            res["roofline"]["traffic_ratio_to_unique_bytes"] = round(traffic / (n * d * 8), 3)
     res["ms_per_step"] = res["one_launch"]["ms_per_step"]
     res["value"] = res["one_launch"]["GB_per_s"]
     del X
@@ -614,6 +622,88 @@ def noised_probe(eng, dev, X, n, d, f, m, k=1):
             "selected_set_same": same_sel, "mean_bitwise_same": same_mean}
 
 
+def _r(x, nd=4):
+    return None if x is None else round(float(x), nd)
+
+
+def _summ(v, host=None):
+    """One config's numbers for the compact line's summary: value (GB/s),
+    ms_per_step, the dominant kernel's roofline frac, PMC traffic over the
+    unique input bytes, selected-set parity and the near-tie flag."""
+    roof = v.get("roofline") or {}
+    par = v.get("parity") or {}
+    if "one_launch" in v:  # small_variant: parity sits with the one-launch timing
+        par = dict(v["one_launch"].get("parity") or {}, **{k: x for k, x in par.items()})
+    traffic = roof.get("traffic")
+    ub = roof.get("unique_bytes")
+    s = {"value": v.get("value"), "ms": v.get("ms_per_step"),
+         "kernel": roof.get("kernel"), "kernel_ms": roof.get("kernel_avg_ms"),
+         "frac": roof.get("frac"), "peak": roof.get("peak"),
+         "traffic_ratio": roof.get("traffic_ratio_to_unique_bytes") or
+         (_r(traffic / ub, 3) if traffic and ub else None),
+         "sel": par.get("selected_set"), "mean": par.get("mean"),
+         "near_tie": (par.get("margin") or {}).get("near_tie")}
+    if "certified_reruns" in v:
+        s["reruns"] = v["certified_reruns"]
+    if host:
+        s["host_ms"] = host.get("ms_per_call")
+        s["host_over_h2d_ms"] = host.get("overhead_over_h2d_ms")
+        s["host_sel"] = (host.get("parity") or {}).get("selected_set")
+    return s
+
+
+def compact_line(out, detail_path):
+    """The printed JSON line: the contract's keys, the headline's roofline,
+    cpu_baseline and parity, and -- as the LAST key -- a per-config summary of
+    every BASELINE config measured in this run, so the driver's stored tail
+    holds all of them.  The full record goes to
+    detail_path (copied under profiles/ for the judged runs)."""
+    try:
+        os.makedirs(os.path.dirname(detail_path), exist_ok=True)
+        with open(detail_path, "w") as fp:
+            json.dump(out, fp, indent=1)
+    except OSError as e:
+        detail_path = "unwritable (%r)" % (e,)
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")
+    line = {k: out[k] for k in keep if k in out}
+    roof = dict(out["roofline"])
+    roof.pop("traffic_source", None)
+    line["roofline"] = roof
+    cb = out.get("cpu_baseline")
+    if cb:
+        line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample",
+                                                    "value_1core", "cpu_model", "error") if k in cb}
+    par = out.get("parity")
+    if par:
+        line["parity"] = par
+    for k in ("step_roofline", "rccl"):
+        if out.get(k):
+            line[k] = out[k]
+    line["detail_file"] = os.path.relpath(detail_path, REPO) if os.path.isabs(detail_path) else detail_path
+    summ = {}
+    head = {"value": out["value"], "ms_per_step": out["ms_per_step"], "roofline": out["roofline"],
+            "parity": out.get("parity")}
+    tag = out["config"]["workload"]
+    if "f32_mode" in out["config"] and out["config"]["f32_mode"] != "exact":
+        tag += "_" + out["config"]["f32_mode"]
+    summ[tag] = _summ(head)
+    for name, v in (out.get("variants") or {}).items():
+        summ[name] = _summ(v, v.get("host_entry"))
+    sc = out.get("single_call")
+    if sc:
+        summ["single_call"] = {"ms": sc["ms"], "k_gram_frac": sc.get("k_gram_frac")}
+    nr = out.get("next_rows")
+    if nr:
+        summ["next_rows"] = {k: {"ms": v.get("ms"), "frac": (v.get("roofline") or {}).get("frac")}
+                             for k, v in nr.items()}
+    e2e = out.get("e2e_pinned_h2d_d2h")
+    if e2e:
+        summ["e2e_pinned"] = {"GB_per_s": e2e["GB_per_s"], "ms": e2e["ms"]}
+    line["summary"] = summ
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -643,6 +733,9 @@ def main():
                     help="N > 1: the packed-Gram exchange inside libbk over RCCL (default), or "
                          "through torch.distributed gloo on the host (bk_gram_upper_device -> "
                          "all_reduce -> bk_finish_device; lets N ranks share one GPU in tests)")
+    ap.add_argument("--detail-out", default=os.path.join(REPO, "gpurun_out", "bench_detail.json"),
+                    help="where the full record goes (every variant, kernel breakdown, probes); "
+                         "the printed line is the compact form with a per-config summary")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="tuning aid on a 1-GPU box: run rank 0's column shard of an N-rank "
                          "job (sharded path, 1-rank RCCL exchange); value is that rank's rate")
@@ -829,6 +922,8 @@ def main():
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
             "kernel": k1name, "kernel_avg_ms": round(g["avg_ms"], 4),
             "flops_per_launch": flops, "events_every": tstride}
+    if traffic:
+        roof["traffic_ratio_to_unique_bytes"] = round(traffic / (n * dl * es), 3)
 
     # the whole step against its floor: t_floor = max(flops_alg / fp64
     # matrix peak, bytes_alg / HBM peak) with bytes_alg = (n + m) * d_local * s + 8 d_local;
@@ -997,7 +1092,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
 
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(compact_line(out, a.detail_out)), flush=True)
     if tdist.is_initialized():
         tdist.barrier()
         tdist.destroy_process_group()

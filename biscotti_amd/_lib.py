@@ -16,7 +16,7 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
-BK_ABI_VERSION = 9
+BK_ABI_VERSION = 10
 BK_F32_EXACT, BK_F32_MFMA, BK_F32_CERTIFIED = 0, 1, 2
 KERNELS = ["k_gram", "k_reduce", "k_transpose", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni",
@@ -61,6 +61,7 @@ SIGNATURES = {
     "bk_timing_read": (_i, [_p, _i, _pd, _pi64]),
     "bk_kernel_name": (ctypes.c_char_p, [_i]),
     "bk_plan": (_i, [_p, _i64, _i64, _pi64, _pi64, _pi64, _pi64]),
+    "bk_plan_mode": (_i, [_p, _i64, _i64, _i, _i, _pi64, _pi64]),
     "bk_aggregate_device": (_i, [_p, _p, _i, _i64, _i64, _i64, _p, _i64, _p]),
     "bk_aggregate": (_i, [_p, _p, _i, _i, _i64, _i64, _i64, _p, _i64, _p]),
     "bk_quantized_sum_device": (_i, [_p, _p, _i, _i64, _i64, _i64, _p, _i64, _i, _p, _p]),

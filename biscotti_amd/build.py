@@ -45,21 +45,35 @@ def needs_build():
 
 
 def build(force=False, verbose=True, extra=(), out=LIB, jobs=None):
-    """extra/out: debug variants (e.g. -DBK_K1_PROBE into tools/ab/), never the product.
+    """extra/out: debug variants (e.g. -DBK_PROBES, -DBK_K1_PROBE into tools/ab/),
+    never the product: the probe knobs (BK_GRAM_MODE, BK_PLAN_*, ...) exist
+    only in a -DBK_PROBES build (bk_internal.h probe_env).
     Each source compiles to its own object in parallel (every kernel is launched
     from its own translation unit, so no relocatable device code is needed),
     then one link."""
     if not force and out == LIB and not needs_build():
         return LIB
-    import concurrent.futures as cf
+    import fcntl
     import hashlib
-    import shutil
     import tempfile
     # a fixed object directory per (output, flags): the object paths end up in
     # the linked library, and a random temp name made every build's sha256
-    # differ (the PMC records are matched to the library by that hash)
+    # differ (the PMC records are matched to the library by that hash).  Two
+    # processes building the same output would delete each other's objects,
+    # so the whole build holds an exclusive lock on that directory's lock file.
     key = hashlib.sha1(("\0".join([out] + list(extra))).encode()).hexdigest()[:12]
     tmp = os.path.join(tempfile.gettempdir(), "bk_build_" + key)
+    with open(tmp + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            return _build_locked(tmp, out, extra, verbose, jobs)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(tmp, out, extra, verbose, jobs):
+    import concurrent.futures as cf
+    import shutil
     shutil.rmtree(tmp, ignore_errors=True)
     os.makedirs(tmp)
     cflags = [f for f in FLAGS if f != "-shared"] + list(extra)
@@ -74,7 +88,8 @@ def build(force=False, verbose=True, extra=(), out=LIB, jobs=None):
     jobs = jobs or min(len(SOURCES), os.cpu_count() or 4, 16)
     with cf.ThreadPoolExecutor(jobs) as ex:
         list(ex.map(compile_one, range(len(SOURCES))))
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"] + LIBS
+    arch = [f for f in FLAGS if f.startswith("--offload-arch=")]
+    cmd = [HIPCC] + arch + ["-shared", "-fPIC"] + objs + ["-o", out + ".tmp"] + LIBS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -407,7 +407,7 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
         double *part = (double *)c->part.p;
         const Plan3 &P3 = *p3;
         long long *trace = nullptr;
-        const char *tfile = getenv("BK_TRACE_FILE");  // debug: per-workgroup timeline
+        const char *tfile = probe_env("BK_TRACE_FILE");  // debug: per-workgroup timeline
         if (tfile) {
             CHK(ensure(c->trace, (size_t)P3.nwg * 24 * sizeof(long long)));
             HIPCHK(hipMemsetAsync(c->trace.p, 0, (size_t)P3.nwg * 24 * sizeof(long long), c->stream));
@@ -553,7 +553,7 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
     const int items = sp.ng + sp.Q + sp.nS + (d_mean ? sp.C : 1);
     const int grid = items < c->num_cu ? items : c->num_cu;  // = launch_small's grid
     const size_t twords = (size_t)items * 8 + (size_t)grid * 2;  // + per workgroup {entry, exit}
-    const char *tfile = getenv("BK_SMALL_TRACE");  // debug: per-item timeline
+    const char *tfile = probe_env("BK_SMALL_TRACE");  // debug: per-item timeline
     if (tfile) {
         CHK(ensure(c->trace, twords * sizeof(long long)));
         HIPCHK(hipMemsetAsync(c->trace.p, 0, twords * sizeof(long long), c->stream));
@@ -824,7 +824,7 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
     }();
     bool zero_copy = false;
     if (where == BK_HOST_PINNED && k == 0 && !noised_out && tiny_zc && tiny_ok((int)n, d) &&
-        !getenv("BK_SMALL_TRACE")) {
+        !probe_env("BK_SMALL_TRACE")) {
         void *hp = nullptr;
         if (hipHostGetDevicePointer(&hp, const_cast<void *>(X), 0) == hipSuccess && hp) {
             dX = hp;
@@ -839,8 +839,12 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
         CHK(ensure(c->X, (size_t)n * dld * es));
         if (k > 0) CHK(ensure(c->noise, (size_t)n * k * d * sizeof(double)));
         CHK(timed(c, BK_K_H2D, [&] {
-            // rows already 16-B multiples (d even for fp64): one linear copy
-            hipError_t e = ld == dld ? hipMemcpyAsync(c->X.p, X, (size_t)n * d * es,
+            // a contiguous batch (ld == d) whose rows are already 16-B
+            // multiples (ld == dld): one linear copy.  A strided caller with
+            // ld == dld != d (a numpy view X[:, :3] of an n x 4 array) takes
+            // the 2-D copy: a linear n * d copy would shift every row after
+            // the first
+            hipError_t e = ld == dld && ld == d ? hipMemcpyAsync(c->X.p, X, (size_t)n * d * es,
                                                       hipMemcpyHostToDevice, c->stream)
                                      : hipMemcpy2DAsync(c->X.p, (size_t)dld * es, X,
                                                         (size_t)ld * es, (size_t)d * es, (size_t)n,
@@ -871,12 +875,23 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
     constexpr size_t MPAD = 16;
     const size_t words = MPAD + 2 * (size_t)n + (mean_out ? (size_t)d : 0);
     if (c->hout_bytes < words * sizeof(double)) {
+        // an earlier asynchronous call's record may be unchecked: if it lives
+        // in the block about to be freed, read it first (its stream is done
+        // once wait_stream returns); a record in the context's own block stays
+        if (c->margin_host && c->margin_host == c->hout_host_margin) {
+            HIPCHK(wait_stream(c));
+            if (c->margin_unchecked) {
+                c->margin_unchecked = 0;
+                CHK(margin_status(c->margin_host));
+            }
+            c->margin_host = nullptr;
+            c->margin_valid = 0;
+        }
         if (c->hout) (void)hipHostFree(c->hout);
         c->hout = nullptr;
         c->hout_bytes = 0;
         c->hout_dev = nullptr;
         c->hout_host_margin = nullptr;
-        c->margin_host = nullptr;
         const size_t bytes = std::max<size_t>(words * sizeof(double), 64 * 1024);
 #ifdef BK_HOUT_COHERENT  // ablation: uncached host block (each store crosses PCIe at once)
         const unsigned hflags = hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent;
@@ -985,7 +1000,7 @@ int bk_create(bk_ctx **out, int device) {
     DeviceGuard dg(device);
     // probe knob: how the host waits for the GPU (hipDeviceScheduleSpin 1,
     // Yield 2, BlockingSync 4; tools/idle_probe.py)
-    if (const char *v = getenv("BK_SCHED")) (void)hipSetDeviceFlags((unsigned)atoi(v));
+    if (const char *v = probe_env("BK_SCHED")) (void)hipSetDeviceFlags((unsigned)atoi(v));
     hipDeviceProp_t prop;
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e == hipSuccess) c->num_cu = prop.multiProcessorCount;
@@ -995,9 +1010,9 @@ int bk_create(bk_ctx **out, int device) {
         return fail(BK_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     c->stream = c->own;
-    if (const char *v = getenv("BK_GRAM"))
+    if (const char *v = probe_env("BK_GRAM"))
         if (strcmp(v, "v1") == 0) c->gram_variant = 1;
-    if (const char *v = getenv("BK_GRAM_MODE")) c->gram_mode = atoi(v);
+    if (const char *v = probe_env("BK_GRAM_MODE")) c->gram_mode = atoi(v);
     if (const char *v = getenv("BK_SMALL")) c->small_on = atoi(v) != 0;
     if (const char *v = getenv("BK_SPIN_US")) c->spin_us = atoll(v);
     // test / debug knobs (tests/test_gpu_errors.py): a hand-off wait that gives
@@ -1116,6 +1131,19 @@ int bk_plan(bk_ctx *c, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *n
     return BK_OK;
 }
 
+int bk_plan_mode(bk_ctx *c, int64_t n, int64_t d, int mode, int rounds, int64_t *S, int64_t *nwg) {
+    if (n < 1 || d < 1) return fail(BK_EINVAL, "need n, d >= 1");
+    if (n > BK_MAX_N) return fail(BK_ENOTSUP, "n=%lld exceeds BK_MAX_N=%d", (long long)n, BK_MAX_N);
+    if (mode < -1 || mode > 3 || rounds < 0 || rounds > 16)
+        return fail(BK_EINVAL, "bad planner mode %d / rounds %d", mode, rounds);
+    const Plan3Host H = build_plan3((int)n, d, c ? c->num_cu : 256, G3_BK, mode, rounds);
+    for (int u = 0; u < H.ntile; ++u)
+        if (H.red[3 * u + 1] < 0) return fail(BK_EHIP, "internal: K1 plan fails its coverage check");
+    if (S) *S = (int64_t)H.groups.size();
+    if (nwg) *nwg = (int64_t)(H.seg.size() / 2);
+    return BK_OK;
+}
+
 namespace {
 
 // The 7-launch step (K1, K1b, K2, K3, K3b, K4) replayed as one hipGraph: the
@@ -1136,6 +1164,11 @@ int run_device_graph(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
         if (cg.X == dX && cg.dtype == dtype && cg.n == n && cg.d == d && cg.ld == ld && cg.f == f &&
             cg.sel == d_sel && cg.scores == d_scores && cg.mean == d_mean) {
             HIPCHK(hipGraphLaunch(cg.exec, c->stream));
+            // the captured finish (K3b / k_small) writes the context's record:
+            // point the readers at it and arm bk_synchronize's check
+            c->margin_valid = 1;
+            c->margin_host = c->hmargin;
+            c->margin_unchecked = 1;
             return BK_OK;
         }
     // eager run first: every ensure() / plan build happens outside the capture
@@ -1182,7 +1215,7 @@ int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t
     if (certified(c, dtype))
         return run_certified(c, [&] { return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean); });
     // (the debug traces synchronize mid-call, which a stream capture refuses)
-    if (c->graph_on && c->timing == 0 && !getenv("BK_TRACE_FILE") && !getenv("BK_SMALL_TRACE"))
+    if (c->graph_on && c->timing == 0 && !probe_env("BK_TRACE_FILE") && !probe_env("BK_SMALL_TRACE"))
         return run_device_graph(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
     return run_device(c, dX, dtype, n, d, ld, f, d_sel, d_scores, d_mean);
 }

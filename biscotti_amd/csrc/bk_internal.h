@@ -3,12 +3,28 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <vector>
 
 #include "bk_synth.h"
 
 namespace bk {
+
+// Probe knobs: timing-only ablations (BK_GRAM_MODE, BK_K2_MODE), planner and
+// kernel-shape overrides and debug traces, read only by A/B builds
+// (build(extra=["-DBK_PROBES"], out=tools/ab/...)).  The product libbk.so
+// never reads them, so no environment variable can make it return a wrong
+// result with BK_OK.  Knobs that only pick between
+// bit-identical paths (BK_TINY, BK_SMALL, BK_STAGE_CHUNK_BYTES) and the test
+// knobs that force a loud failure stay in the product.
+#ifdef BK_PROBES
+inline const char *probe_env(const char *name) { return getenv(name); }
+constexpr bool kProbes = true;
+#else
+inline const char *probe_env(const char *) { return nullptr; }
+constexpr bool kProbes = false;
+#endif
 
 // Split-K plan of K1 for one (n, d): T = ceil(n/64) sub-tile rows, ntile =
 // T(T+1)/2 upper sub-tiles, S k-pieces of kc columns (multiple of 8), one wave
@@ -68,7 +84,9 @@ struct Plan3Host {
     std::vector<int> wglist;  // concatenated per-group workgroup lists
 };
 // bk = columns per k-block: 16 for fp64 input, 32 for fp32 (128 B per row either way)
-Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk = G3_BK);
+// mode / rounds >= 0 / > 0: force a planner mode (0 v7, 1 v8 strides, 2 McNaughton,
+// 3 aligned pieces) and round count (bk_plan_mode); -1 / 0: the planner's choice
+Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk = G3_BK, int mode = -1, int rounds = 0);
 
 // K1 v3: one launched workgroup runs its segments one after the other (a CU's
 // share of the columns may span two groups: bk_plan.hip "McNaughton")

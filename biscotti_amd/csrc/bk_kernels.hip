@@ -1689,25 +1689,30 @@ static int next_pow2(int v) {
 template <int NT, int KPT, int NT_SUM, bool TR>
 static void launch_scores2(const double *U, const double *Ut, const double *dg, int T, int n, int N,
                            int64_t k, double *scores, double *diag, hipStream_t st) {
-    static const int mode = [] {
-        const char *e = getenv("BK_K2_MODE");  // timing-only ablations (tools/), never tests
-        return e ? atoi(e) : 0;
-    }();
     const size_t lds = (size_t)(KPT == 16 ? N + N / 16 : N) * sizeof(uint64_t);  // v3: padded
-    if (mode == 1)
-        hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 1>), dim3(n), dim3(NT), lds, st, U, Ut,
-                           dg, T, n, N, k, scores, diag);
-    else if (mode == 2)
-        hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 2>), dim3(n), dim3(NT), lds, st, U, Ut,
-                           dg, T, n, N, k, scores, diag);
-    else
-        hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR>), dim3(n), dim3(NT), lds, st, U, Ut, dg,
-                           T, n, N, k, scores, diag);
+    if constexpr (kProbes) {  // timing-only ablations (tools/k2_modes.py): probe builds only
+        static const int mode = [] {
+            const char *e = probe_env("BK_K2_MODE");
+            return e ? atoi(e) : 0;
+        }();
+        if (mode == 1) {
+            hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 1>), dim3(n), dim3(NT), lds, st, U,
+                               Ut, dg, T, n, N, k, scores, diag);
+            return;
+        }
+        if (mode == 2) {
+            hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 2>), dim3(n), dim3(NT), lds, st, U,
+                               Ut, dg, T, n, N, k, scores, diag);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR>), dim3(n), dim3(NT), lds, st, U, Ut, dg, T,
+                       n, N, k, scores, diag);
 }
 
 bool scores_transposed(int n) {
     static const int tmin = [] {
-        const char *e = getenv("BK_K2_TRANSPOSE_MIN_N");  // probe knob
+        const char *e = probe_env("BK_K2_TRANSPOSE_MIN_N");  // probe knob
         return e ? atoi(e) : 2049;
     }();
     return n >= tmin;
@@ -1724,11 +1729,11 @@ hipError_t launch_scores(const double *U, const double *Ut, const double *dg, in
     const int np2 = next_pow2(n < 2 ? 2 : n);
     const size_t lds = (size_t)np2 * sizeof(uint64_t);
     static const bool v1 = [] {
-        const char *e = getenv("BK_SCORES");
+        const char *e = probe_env("BK_SCORES");
         return e && strcmp(e, "v1") == 0;
     }();
     static const int kpt_big = [] {  // probe knob: keys per thread above 2048 keys
-        const char *e = getenv("BK_K2_KPT");
+        const char *e = probe_env("BK_K2_KPT");
         return e ? atoi(e) : 16;
     }();
     if (!v1) {
@@ -1908,7 +1913,9 @@ hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, i
 
 hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl,
                         double *part, hipStream_t st, int mode, long long *trace, bool f32_mfma) {
-    // mode != 0: timing-only ablations (1: no MFMA, 2: no global loads) -- wrong results
+    // mode != 0: timing-only ablations (1: no MFMA, 2: no global loads) -- wrong
+    // results, so they exist only in probe builds (-DBK_PROBES); the product ignores mode
+    (void)mode;
     const dim3 grid((unsigned)pl.nwg), block(512);
     if (dtype != 0 && f32_mfma)  // fp32 input on the fp32 MFMA
         hipLaunchKernelGGL((k_gram3<0, f32m>), grid, block, G3_LDS, st, (const f32m *)X, ld, n,
@@ -1916,12 +1923,14 @@ hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     else if (dtype != 0)  // fp32 input, exact (widened onto the fp64 MFMA): production mode only
         hipLaunchKernelGGL((k_gram3<0, float>), grid, block, G3_LDS, st, (const float *)X, ld, n,
                            pl.nfull, d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
+#ifdef BK_PROBES
     else if (mode == 1)
         hipLaunchKernelGGL(k_gram3<1>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
                            d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
     else if (mode == 2)
         hipLaunchKernelGGL(k_gram3<2>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
                            d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
+#endif
     else
         hipLaunchKernelGGL(k_gram3<0>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
                            d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
@@ -1943,12 +1952,17 @@ hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStr
 }
 
 hipError_t configure_kernels() {
-    for (const void *k : {(const void *)k_gram3<0>, (const void *)k_gram3<1>,
-                          (const void *)k_gram3<2>, (const void *)k_gram3<0, float>,
+    for (const void *k : {(const void *)k_gram3<0>, (const void *)k_gram3<0, float>,
                           (const void *)k_gram3<0, f32m>}) {
         hipError_t e0 = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
         if (e0 != hipSuccess) return e0;
     }
+#ifdef BK_PROBES
+    for (const void *k : {(const void *)k_gram3<1>, (const void *)k_gram3<2>}) {
+        hipError_t e0 = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
+        if (e0 != hipSuccess) return e0;
+    }
+#endif
     // the row sort may need up to BK_MAX_N * 8 = 128 KiB of dynamic LDS
     hipError_t e = hipFuncSetAttribute((const void *)k_scores<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
@@ -1964,6 +1978,7 @@ hipError_t configure_kernels() {
                            (const void *)k_scores2<512, 16, 1024, true>,
                            (const void *)k_scores2<1024, 16, 1024, true>,
                            (const void *)k_scores2<1024, 4, 1024, true>,
+#ifdef BK_PROBES  // the timing-only K2 ablations (BK_K2_MODE)
                            (const void *)k_scores2<256, 16, 1024, false, 1>,
                            (const void *)k_scores2<512, 16, 1024, false, 1>,
                            (const void *)k_scores2<1024, 16, 1024, false, 1>,
@@ -1979,7 +1994,9 @@ hipError_t configure_kernels() {
                            (const void *)k_scores2<256, 16, 1024, true, 2>,
                            (const void *)k_scores2<512, 16, 1024, true, 2>,
                            (const void *)k_scores2<1024, 16, 1024, true, 2>,
-                           (const void *)k_scores2<1024, 4, 1024, true, 2>}) {
+                           (const void *)k_scores2<1024, 4, 1024, true, 2>,
+#endif
+                       }) {
         e = hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, 144 * 1024);  // v3 at N = 16384: 136 KiB
         if (e != hipSuccess) return e;
     }

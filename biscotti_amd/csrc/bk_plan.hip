@@ -29,7 +29,7 @@ constexpr int COST_OFF = 16, COST_PAIR = 20, COST_DIAG1 = 10;
 // they set how the planner splits an XCD's columns between groups so that all
 // its CUs finish together.
 double eff_cost(const GroupDesc &g) {
-    const char *v = getenv("BK_PLAN_NB_COST");
+    const char *v = probe_env("BK_PLAN_NB_COST");
     const double b = v ? atof(v) : 0.37;
     return 1.015 * g.cost + b * g.nb;
 }
@@ -149,7 +149,7 @@ std::vector<std::vector<Piece>> mcnaughton(const std::vector<double> &e, int64_t
 
 }  // namespace
 
-Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
+Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk, int mode_in, int rounds_in) {
     Plan3Host H;
     const int T = (n + 63) / 64;
     const int TT = (T + 1) / 2;  // 128-row super-blocks
@@ -197,7 +197,7 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
         // wave 0, slab 0), 7 = (2I+1, 2I+3) tile 2I+1 (A, wave 0 slab 1),
         // 6 = (2I+1, 2I+2) tile 2I+2 (B, wave 1 slab 0), 3 = (2I, 2I+3) tile
         // 2I+3 (B, wave 1 slab 1).  Same MFMAs in the same order: bitwise equal.
-        const char *eb = getenv("BK_QUAD_BAL");
+        const char *eb = probe_env("BK_QUAD_BAL");
         const bool full = w[0].kind == T_PAIR && w[1].kind == T_PAIR && st.size() == 4;
         if (full && !(eb && atoi(eb) == 0)) {
             w[0].xt = w[1].xt = 1;
@@ -279,17 +279,18 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk) {
     for (int x = 0; x <= NX; ++x) K[x] = (int64_t)nfull * x / NX;
     // prologue (ring fill at loaded latency) + partial-slab write + reduce share,
     // in cost units (256 shader cycles): ~10 us per workgroup
-    const char *ev = getenv("BK_PLAN_WGOH");
+    const char *ev = probe_env("BK_PLAN_WGOH");
     const double wg_overhead = ev ? atof(ev) : 100.0;
-    const char *er = getenv("BK_PLAN_ROUNDS");
-    const int force_rounds = er ? atoi(er) : 0;
+    const char *er = probe_env("BK_PLAN_ROUNDS");
+    const int force_rounds = rounds_in > 0 ? rounds_in : er ? atoi(er) : 0;
     // McNaughton where an XCD has at least as many CUs as groups (n <= 1024:
     // D -2.2%, its 8-GPU shard -2.0%, C -0.5% against v8); with more groups
     // (n = 4096: 256) each slot would run ~8 whole groups back to back, and
     // v8's one workgroup per group, handed to CUs as they free up, absorbs the
     // CUs' speed spread better (+3.3% for McNaughton there)
     int mode = ng <= per_xcd ? 2 : 1;
-    if (const char *em = getenv("BK_PLAN_MODE")) mode = atoi(em);
+    if (const char *em = probe_env("BK_PLAN_MODE")) mode = atoi(em);
+    if (mode_in >= 0) mode = mode_in;  // bk_plan_mode (the planner's coverage test)
     std::vector<double> eg(ng);
     for (int g = 0; g < ng; ++g) eg[g] = eff_cost(G[g]);
     auto slab_of = [&](int g) {

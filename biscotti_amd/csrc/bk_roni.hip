@@ -35,7 +35,7 @@ namespace bk {
 // A/B knob: BK_RONI_VALU=1 runs the r3a VALU kernels (K7 for d <= 1024, K8)
 static bool roni_valu() {
     static const bool v = [] {
-        const char *e = getenv("BK_RONI_VALU");
+        const char *e = probe_env("BK_RONI_VALU");
         return e && atoi(e) != 0;
     }();
     return v;
@@ -675,7 +675,7 @@ hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, con
     // sample tiles per workgroup (8; BK_RONI_TILES for A/B): more, shorter
     // workgroups hide each tile's barrier and LDS latency behind the others
     static const int per_env = [] {
-        const char *e = getenv("BK_RONI_TILES");
+        const char *e = probe_env("BK_RONI_TILES");
         const int v = e ? atoi(e) : 0;
         return v >= 1 && v <= 256 ? v : 8;
     }();

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 9
+#define BK_ABI_VERSION 10
 
 typedef struct bk_ctx bk_ctx;
 
@@ -398,6 +398,14 @@ const char *bk_kernel_name(int kernel_id);
  * nwg = workgroups of the launch.  Host-side only; ctx may be NULL. */
 int bk_plan(bk_ctx *ctx, int64_t n, int64_t d, int64_t *S, int64_t *kc, int64_t *ntile,
             int64_t *nwg);
+/* The same plan with the planner's mode forced (0: v7 interleave, 1: v8
+ * round-aligned strides, 2: McNaughton pieces, 3: aligned pieces; -1: the
+ * planner's own choice) and its round count (0: the planner's choice).  Every
+ * mode computes the same Gram; this entry exists so the planner's coverage
+ * check can be exercised for all of them (tests/test_abi.py).  Host-side
+ * only; ctx may be NULL.  BK_EHIP if the plan fails its coverage check. */
+int bk_plan_mode(bk_ctx *ctx, int64_t n, int64_t d, int mode, int rounds, int64_t *S,
+                 int64_t *nwg);
 
 #ifdef __cplusplus
 }

@@ -41,7 +41,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_names():
     L = _lib.lib()
-    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 9
+    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 10
     assert L.bk_kernel_name(0) == b"k_gram"
     assert L.bk_kernel_name(99) == b"?"
     assert len(_lib.KERNELS) == 16
@@ -87,20 +87,30 @@ def test_plan_fills_the_chip():
 
 @pytest.mark.parametrize("mode,rounds", [("2", ""), ("1", ""), ("0", ""), ("3", ""), ("3", "4"),
                                          ("2", "8")])
-def test_plan_covers_every_kblock_once(mode, rounds, monkeypatch):
+def test_plan_covers_every_kblock_once(mode, rounds):
     """The planner's own check (bk_plan.hip): every (group, k-block) pair is
     owned by exactly one workgroup and every group has one ragged-tail
     workgroup -- for McNaughton pieces (default), the v8 round-aligned strides,
-    the v7 interleave and the aligned pieces (BK_PLAN_MODE), over shapes from
+    the v7 interleave and the aligned pieces (bk_plan_mode), over shapes from
     tiny to BK_MAX_N."""
-    monkeypatch.setenv("BK_PLAN_MODE", mode)
-    if rounds:
-        monkeypatch.setenv("BK_PLAN_ROUNDS", rounds)
     L = _lib.lib()
-    v = [ctypes.c_int64() for _ in range(4)]
+    v = [ctypes.c_int64() for _ in range(2)]
     for n, d in [(1, 1), (2, 16), (65, 100), (100, 7850), (300, 1000003), (512, 1 << 20),
                  (512, 131072), (1000, 12345), (4096, 32768), (16384, 4096)]:
-        assert L.bk_plan(None, n, d, *[ctypes.byref(x) for x in v]) == 0, (n, d, _lib.last_error())
+        assert L.bk_plan_mode(None, n, d, int(mode), int(rounds or 0),
+                              *[ctypes.byref(x) for x in v]) == 0, (n, d, _lib.last_error())
+
+
+def test_probe_knobs_are_not_in_the_product():
+    """The timing-only ablations and planner overrides (BK_GRAM_MODE,
+    BK_K2_MODE, BK_PLAN_*, ...) are compiled only into -DBK_PROBES builds:
+    the product library does not even contain their names."""
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for knob in (b"BK_GRAM_MODE", b"BK_K2_MODE", b"BK_PLAN_MODE", b"BK_PLAN_ROUNDS",
+                 b"BK_PLAN_NB_COST", b"BK_PLAN_WGOH", b"BK_QUAD_BAL", b"BK_K2_KPT",
+                 b"BK_K2_TRANSPOSE_MIN_N", b"BK_SCHED", b"BK_SCORES", b"BK_RONI_VALU",
+                 b"BK_RONI_TILES", b"BK_TRACE_FILE", b"BK_SMALL_TRACE"):
+        assert knob not in blob, knob
 
 
 def test_null_and_bad_arguments_do_not_crash():

@@ -87,3 +87,27 @@ def test_timing_bypasses_graph(engine, graph_engine):
     graph_engine.timing_enable(False)
     assert _same(got, ref)
     assert t["k_small"]["count"] == 1  # n <= 128: the one-launch path, evented
+
+
+def test_replay_after_host_small_call_reports_its_own_margin(graph_engine, oracle):
+    """a replayed device call must point the margin readers
+    at the record its captured finish writes, and arm bk_synchronize's check --
+    not leave them on an earlier host call's output block."""
+    n, d, f = 100, 7850, 30
+    X, sel, sc, mean = _bufs(n, d, f)
+    graph_engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 21, f)
+    for _ in range(3):  # eager, capture, replay
+        _call(graph_engine, X, sel, sc, mean, f)
+    rec_dev = graph_engine.selection_margin()
+    # a host call of another batch: its record lands in the host output block
+    Xh = oracle.synth(90, 333, 5, 20)
+    hs, _, _ = graph_engine.multikrum(Xh, 20)
+    assert np.array_equal(hs, oracle.krum(Xh, 20)[0])
+    rec_host = graph_engine.selection_margin()
+    assert rec_host["d"] == 333 and rec_host["k"] == 90 - 20 - 2
+    # the replayed device call again: its own record, not the host call's
+    got = _call(graph_engine, X, sel, sc, mean, f)
+    rec = graph_engine.selection_margin()
+    assert rec["d"] == d and rec["k"] == n - f - 2
+    assert rec == rec_dev
+    assert np.array_equal(got[0], oracle.krum(X.cpu().numpy(), f)[0])

@@ -181,3 +181,24 @@ def test_host_entry_writes_outputs_in_place(engine, oracle, n, d, f, dtype):
     engine.multikrum(Xh, f)
     assert engine.selection_margin() == hmg
     assert omg != hmg
+
+
+@pytest.mark.parametrize("dtype,n,d,ld,f", [
+    (np.float64, 12, 3, 4, 4),         # a numpy view X[:, :3] of an n x 4 array: ld == dld != d
+    (np.float64, 100, 7849, 7850, 30),  # mnist-sized, odd d
+    (np.float32, 20, 6, 8, 5),
+    (np.float32, 64, 1021, 1024, 20),
+    (np.float64, 10, 25, 26, 2)])       # config A's shape (k_tiny), padded
+def test_host_small_strided_view(engine, oracle, dtype, n, d, ld, f):
+    """the host entry of the n <= 128 path with ld equal to
+    the 16-B-rounded d but d itself shorter.  The batch must cross as a 2-D
+    copy; a linear n*d copy shifted every row after the first."""
+    full = oracle.synth(n, ld, 900 + n + d, f, dtype=dtype)
+    Xv = full[:, :d]
+    assert Xv.strides[0] // Xv.itemsize == ld
+    sel, sc, mean = engine.multikrum(Xv, f)
+    osel, osc, omean = oracle.krum(np.ascontiguousarray(Xv), f)
+    assert np.array_equal(sel, osel)
+    assert np.max(np.abs(sc - osc)) <= 1e-9 * max(1e-300, np.max(np.abs(osc)))
+    mscale = float(np.max(np.mean(np.abs(Xv[osel].astype(np.float64)), axis=0)))
+    assert np.max(np.abs(mean - omean)) <= 1e-9 * max(mscale, 1e-300)

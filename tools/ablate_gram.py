@@ -8,6 +8,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from biscotti_amd import _lib  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import probe_build  # noqa: E402
+probe_build.use(_lib)  # probe knobs live in the -DBK_PROBES build only
 from biscotti_amd.krum import Engine  # noqa: E402
 
 n, d = int(os.environ.get("N", 512)), int(os.environ.get("D", 1 << 20))

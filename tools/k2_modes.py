@@ -5,6 +5,9 @@ if len(sys.argv) > 1:
     import torch
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from biscotti_amd import _lib
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import probe_build
+    probe_build.use(_lib)  # probe knobs live in the -DBK_PROBES build only
     from biscotti_amd.krum import Engine
     eng = Engine(0)
     for (n, d, f, dt, tdt) in [(4096, 8192, 1228, _lib.BK_F32, torch.float32), (512, 65536, 153, _lib.BK_F64, torch.float64), (100, 7850, 30, _lib.BK_F64, torch.float64)]:

@@ -14,8 +14,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     import torch
     from biscotti_amd import _lib
-    if os.environ.get("LIB"):  # an A/B build (biscotti_amd.build.build(out=...))
-        _lib.LIB_PATH = os.path.abspath(os.environ["LIB"])
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import probe_build  # noqa: E402
+    probe_build.use(_lib)  # probe knobs live in the -DBK_PROBES build only
     from biscotti_amd._lib import check, lib
     from biscotti_amd.krum import Engine
     eng = Engine(0)

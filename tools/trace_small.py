@@ -7,8 +7,9 @@ if sys.argv[1] == "run":
     import torch
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from biscotti_amd import _lib
-    if os.environ.get("LIB"):  # another build, e.g. build_ab/libbk_nt512.so
-        _lib.LIB_PATH = os.path.abspath(os.environ["LIB"])
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import probe_build  # noqa: E402
+    probe_build.use(_lib)  # probe knobs live in the -DBK_PROBES build only
     from biscotti_amd.krum import Engine
     tf = os.environ["BK_SMALL_TRACE"]
     if os.path.exists(tf):
