@@ -399,12 +399,27 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
     wm = torch.randn(cm * (dinm + 1), dtype=torch.float64, device=dev, generator=g2) * 0.05
     dm = torch.randn((nrm, cm * (dinm + 1)), dtype=torch.float64, device=dev, generator=g2) * 1e-3
     rsm = torch.empty(nrm, dtype=torch.float64, device=dev)
+    ntm = torch.empty(2 * nrm + 1, dtype=torch.int32, device=dev)
     runs["k_roni_softmax"] = (
         lambda: check(lib().bk_roni_softmax_device(eng.ctx, Xm.data_ptr(), nvm, dinm, dinm,
                                                    ym.data_ptr(), cm, wm.data_ptr(), dm.data_ptr(),
-                                                   nrm, cm * (dinm + 1), rsm.data_ptr())),
-        None, "softmax RONI scores of %d updates (d = %d) on %d x %d fp32 samples, %d classes "
-              "(ML/Pytorch/client_obj.py:100-112)" % (nrm, cm * (dinm + 1), nvm, dinm, cm))
+                                                   nrm, cm * (dinm + 1), rsm.data_ptr(),
+                                                   ntm.data_ptr())),
+        None, "softmax RONI scores of %d updates (d = %d), every evaluation over the whole "
+              "%d x %d fp32 set, %d classes (ML/Pytorch/client_obj.py:100-112 with batch_size "
+              ">= nv)" % (nrm, cm * (dinm + 1), nvm, dinm, cm))
+    # the reference's own semantics (client.py:136-144): each update's original and
+    # after errors on two random last mini-batches of batch_size 10 (honest.go:47)
+    nbm = 10
+    im = torch.randint(0, nvm, (nrm, 2, nbm), dtype=torch.int64, device=dev, generator=g2)
+    runs["k_roni_softmax_batches"] = (
+        lambda: check(lib().bk_roni_softmax_batches_device(
+            eng.ctx, Xm.data_ptr(), nvm, dinm, dinm, ym.data_ptr(), cm, wm.data_ptr(),
+            dm.data_ptr(), nrm, cm * (dinm + 1), im.data_ptr(), nbm, rsm.data_ptr(),
+            ntm.data_ptr())),
+        nrm * cm * (dinm + 1) * 8 + 2 * nrm * nbm * dinm * 4 + cm * (dinm + 1) * 8,
+        "softmax RONI of %d updates (d = %d), each on its two last mini-batches of %d "
+        "samples (client.py:136-144)" % (nrm, cm * (dinm + 1), nbm))
     res = {}
     for name, (fn, nbytes, what) in runs.items():
         fn()
@@ -416,7 +431,7 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
         t = eng.timing_read().get("k_roni" if name.startswith("k_roni") else name)
         eng.timing_enable(False)
         ms = t["avg_ms"]
-        if name.startswith("k_roni"):  # fp64 MFMA GEMMs (r3b): algorithmic flops
+        if name.startswith("k_roni") and nbytes is None:  # fp64 MFMA GEMMs: algorithmic flops
             if name == "k_roni_softmax":  # nv x (n+1) x C x d_in
                 fl, nu = 2.0 * nvm * (nrm + 1) * cm * dinm, nrm
             else:  # nv x (n+1) x d

@@ -71,9 +71,13 @@ SIGNATURES = {
     "bk_roni_device": (_i, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _i64, _i64, _p]),
     "bk_roni_set_validation": (_i, [_p, _p, _i64, _i64, _i64, _p]),
     "bk_roni": (_i, [_p, _p, _p, _i64, _i64, _i64, _p]),
-    "bk_roni_softmax_device": (_i, [_p, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _i64, _i64, _p]),
+    "bk_roni_softmax_device": (_i, [_p, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _i64, _i64, _p,
+                                    _p]),
+    "bk_roni_softmax_batches_device": (_i, [_p, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _i64,
+                                            _i64, _p, _i64, _p, _p]),
     "bk_roni_softmax_set_validation": (_i, [_p, _p, _i64, _i64, _i64, _p, _i64]),
-    "bk_roni_softmax": (_i, [_p, _p, _p, _i64, _i64, _p]),
+    "bk_roni_softmax": (_i, [_p, _p, _p, _i64, _i64, _p, _p]),
+    "bk_roni_softmax_batches": (_i, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _p]),
     "bk_group_create": (_i, [ctypes.POINTER(_p), _i, _p, _i]),
     "bk_group_destroy": (None, [_p]),
     "bk_group_size": (_i, [_p]),

@@ -116,7 +116,7 @@ struct bk_ctx {
     int64_t roni_nv = 0, roni_dim = 0;
     // the torch-path (softmax) RONI: its validation set (fp32 samples, int32
     // labels; bk_roni_softmax_set_validation) and the prepared models
-    DevBuf rmc_X, rmc_y, rmc_ws;
+    DevBuf rmc_X, rmc_y, rmc_ws, rmc_xn, rmc_idx, rmc_nt;
     int64_t rmc_nv = 0, rmc_din = 0, rmc_C = 0;
     // bk_multikrum_noised: a 2-slot ring of noise chunks, filled on a copy
     // stream while K6 consumes the previous chunk on `stream` (created lazily)
@@ -212,7 +212,8 @@ void bind_epoch(bk_ctx *c) {
                       &c->X,    &c->mean, &c->perm, &c->trace,  &c->idx,    &c->roni_X,
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                       &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
-                      &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws};
+                      &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws,
+                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -1046,7 +1047,8 @@ void bk_destroy(bk_ctx *c) {
                           &c->mask, &c->sel,  &c->X,   &c->mean, &c->perm, &c->trace, &c->idx,
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                           &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
-                          &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws};
+                          &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws,
+                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt};
         if (c->hmargin) (void)hipHostFree(c->hmargin);
         if (c->hout) (void)hipHostFree(c->hout);
         if (c->copy) (void)hipStreamSynchronize(c->copy);
@@ -2215,7 +2217,8 @@ static int check_roni_softmax(int64_t nv, int64_t din, int64_t ldv, int64_t C, i
 
 int bk_roni_softmax_device(bk_ctx *c, const float *d_Xv, int64_t nv, int64_t d_in, int64_t ldv,
                            const int32_t *d_yv, int64_t n_classes, const double *d_ww,
-                           const double *d_deltas, int64_t n, int64_t ld, double *d_scores) {
+                           const double *d_deltas, int64_t n, int64_t ld, double *d_scores,
+                           int32_t *d_near_ties) {
     if (!c) return fail(BK_EINVAL, "null context");
     CHK(check_roni_softmax(nv, d_in, ldv, n_classes, n, ld));
     if (!d_Xv || !d_yv || !d_ww || (n > 0 && (!d_deltas || !d_scores)))
@@ -2224,11 +2227,32 @@ int bk_roni_softmax_device(bk_ctx *c, const float *d_Xv, int64_t nv, int64_t d_i
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     CHK(ensure(c->rmc_ws, roni_softmax_ws(n, d_in, nv, (int)n_classes)));
-    CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
+    CHK(ensure(c->roni_cnt, (size_t)2 * (n + 1) * sizeof(unsigned int)));
     return timed(c, BK_K_RONI, [&] {
         return launch_roni_softmax(d_Xv, nv, d_in, ldv, d_yv, (int)n_classes, d_ww, d_deltas, n,
-                                   ld, (double *)c->rmc_ws.p, (unsigned int *)c->roni_cnt.p,
-                                   d_scores, c->stream);
+                                   ld, (double *)c->rmc_ws.p, nullptr, (unsigned int *)c->roni_cnt.p,
+                                   d_scores, d_near_ties, c->stream);
+    });
+}
+
+int bk_roni_softmax_batches_device(bk_ctx *c, const float *d_Xv, int64_t nv, int64_t d_in,
+                                   int64_t ldv, const int32_t *d_yv, int64_t n_classes,
+                                   const double *d_ww, const double *d_deltas, int64_t n,
+                                   int64_t ld, const int64_t *d_idx, int64_t nb, double *d_scores,
+                                   int32_t *d_near_ties) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    CHK(check_roni_softmax(nv, d_in, ldv, n_classes, n, ld));
+    if (nb < 1) return fail(BK_EINVAL, "need a batch of nb >= 1 samples (nb=%lld)", (long long)nb);
+    if (n > 0x7fffffff) return fail(BK_ENOTSUP, "RONI n=%lld exceeds the grid", (long long)n);
+    if (!d_Xv || !d_yv || !d_ww || (n > 0 && (!d_deltas || !d_scores || !d_idx)))
+        return fail(BK_EINVAL, "null pointer argument");
+    if (n == 0) return BK_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    return timed(c, BK_K_RONI, [&] {
+        return launch_roni_softmax_batches(d_Xv, nv, d_in, ldv, d_yv, (int)n_classes, d_ww,
+                                           d_deltas, n, ld, d_idx, nb, d_scores, d_near_ties,
+                                           c->stream);
     });
 }
 
@@ -2243,10 +2267,14 @@ int bk_roni_softmax_set_validation(bk_ctx *c, const float *Xv, int64_t nv, int64
     HostDrain drain{c};
     CHK(ensure(c->rmc_X, (size_t)nv * d_in * sizeof(float)));
     CHK(ensure(c->rmc_y, (size_t)nv * sizeof(int32_t)));
+    CHK(ensure(c->rmc_xn, (size_t)nv * sizeof(double)));
     HIPCHK(hipMemcpy2DAsync(c->rmc_X.p, (size_t)d_in * sizeof(float), Xv, (size_t)ldv * sizeof(float),
                             (size_t)d_in * sizeof(float), (size_t)nv, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->rmc_y.p, yv, (size_t)nv * sizeof(int32_t), hipMemcpyHostToDevice,
                           c->stream));
+    // the samples' norms (the near-tie bound), once per validation set
+    HIPCHK(launch_roni_xnorm((const float *)c->rmc_X.p, nv, d_in, d_in, (double *)c->rmc_xn.p,
+                             c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     drain.armed = false;
     c->rmc_nv = nv;
@@ -2255,23 +2283,40 @@ int bk_roni_softmax_set_validation(bk_ctx *c, const float *Xv, int64_t nv, int64
     return BK_OK;
 }
 
-int bk_roni_softmax(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_t ld,
-                    double *scores) {
+// the host forms: ww / deltas (and the batches' indices) to the device, K8,
+// scores and near-tie counts back; synchronous
+static int roni_softmax_host(bk_ctx *c, const double *ww, const double *deltas, int64_t n,
+                             int64_t ld, const int64_t *idx, int64_t nb, double *scores,
+                             int32_t *near_ties) {
     if (!c) return fail(BK_EINVAL, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->rmc_nv < 1) return fail(BK_EINVAL, "no validation set: call bk_roni_softmax_set_validation");
-    const int64_t din = c->rmc_din, C = c->rmc_C, d = C * (din + 1);
-    CHK(check_roni_softmax(c->rmc_nv, din, din, C, n, ld));
+    const int64_t nv = c->rmc_nv, din = c->rmc_din, C = c->rmc_C, d = C * (din + 1);
+    CHK(check_roni_softmax(nv, din, din, C, n, ld));
     if (!ww || (n > 0 && (!deltas || !scores))) return fail(BK_EINVAL, "null pointer argument");
+    if (idx) {
+        if (nb < 1) return fail(BK_EINVAL, "need a batch of nb >= 1 samples (nb=%lld)", (long long)nb);
+        if (n > 0x7fffffff) return fail(BK_ENOTSUP, "RONI n=%lld exceeds the grid", (long long)n);
+        for (int64_t i = 0; i < 2 * n * nb; ++i)
+            if (idx[i] < 0 || idx[i] >= nv)
+                return fail(BK_EINVAL, "batch index %lld = %lld outside [0, %lld)", (long long)i,
+                            (long long)idx[i], (long long)nv);
+    }
     if (n == 0) return BK_OK;
     DeviceGuard dg(c->device);
     HostDrain drain{c};  // error returns: queued H2D copies may still read ww / deltas
+    const int64_t nnt = idx ? 2 * n : n + 1;
     CHK(ensure(c->roni_w, (size_t)d * sizeof(double)));
     CHK(ensure(c->roni_d, (size_t)n * d * sizeof(double)));
     CHK(ensure(c->roni_s, (size_t)n * sizeof(double)));
-    CHK(ensure(c->rmc_ws, roni_softmax_ws(n, din, c->rmc_nv, (int)C)));
-    CHK(ensure(c->roni_cnt, (size_t)(n + 1) * sizeof(unsigned int)));
+    CHK(ensure(c->rmc_nt, (size_t)nnt * sizeof(int32_t)));
+    if (idx) CHK(ensure(c->rmc_idx, (size_t)2 * n * nb * sizeof(int64_t)));
+    if (!idx) {
+        CHK(ensure(c->rmc_ws, roni_softmax_ws(n, din, nv, (int)C)));
+        CHK(ensure(c->roni_cnt, (size_t)2 * (n + 1) * sizeof(unsigned int)));
+    }
     double *dw = (double *)c->roni_w.p, *dd = (double *)c->roni_d.p, *ds = (double *)c->roni_s.p;
+    int32_t *dnt = (int32_t *)c->rmc_nt.p;
     CHK(timed(c, BK_K_H2D, [&] {
         hipError_t e = hipMemcpyAsync(dw, ww, (size_t)d * sizeof(double), hipMemcpyHostToDevice,
                                       c->stream);
@@ -2279,19 +2324,43 @@ int bk_roni_softmax(bk_ctx *c, const double *ww, const double *deltas, int64_t n
             e = hipMemcpy2DAsync(dd, (size_t)d * sizeof(double), deltas, (size_t)ld * sizeof(double),
                                  (size_t)d * sizeof(double), (size_t)n, hipMemcpyHostToDevice,
                                  c->stream);
+        if (e == hipSuccess && idx)
+            e = hipMemcpyAsync(c->rmc_idx.p, idx, (size_t)2 * n * nb * sizeof(int64_t),
+                               hipMemcpyHostToDevice, c->stream);
         return e;
     }));
     CHK(timed(c, BK_K_RONI, [&] {
-        return launch_roni_softmax((const float *)c->rmc_X.p, c->rmc_nv, din, din,
+        if (idx)
+            return launch_roni_softmax_batches((const float *)c->rmc_X.p, nv, din, din,
+                                               (const int32_t *)c->rmc_y.p, (int)C, dw, dd, n, d,
+                                               (const int64_t *)c->rmc_idx.p, nb, ds, dnt,
+                                               c->stream);
+        return launch_roni_softmax((const float *)c->rmc_X.p, nv, din, din,
                                    (const int32_t *)c->rmc_y.p, (int)C, dw, dd, n, d,
-                                   (double *)c->rmc_ws.p, (unsigned int *)c->roni_cnt.p, ds,
-                                   c->stream);
+                                   (double *)c->rmc_ws.p, (const double *)c->rmc_xn.p,
+                                   (unsigned int *)c->roni_cnt.p, ds, dnt, c->stream);
     }));
     CHK(timed(c, BK_K_D2H, [&] {
-        return hipMemcpyAsync(scores, ds, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
-                              c->stream);
+        hipError_t e = hipMemcpyAsync(scores, ds, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
+                                      c->stream);
+        if (e == hipSuccess && near_ties)
+            e = hipMemcpyAsync(near_ties, dnt, (size_t)nnt * sizeof(int32_t),
+                               hipMemcpyDeviceToHost, c->stream);
+        return e;
     }));
     HIPCHK(hipStreamSynchronize(c->stream));
     drain.armed = false;
     return BK_OK;
+}
+
+int bk_roni_softmax(bk_ctx *c, const double *ww, const double *deltas, int64_t n, int64_t ld,
+                    double *scores, int32_t *near_ties) {
+    return roni_softmax_host(c, ww, deltas, n, ld, nullptr, 0, scores, near_ties);
+}
+
+int bk_roni_softmax_batches(bk_ctx *c, const double *ww, const double *deltas, int64_t n,
+                            int64_t ld, const int64_t *idx, int64_t nb, double *scores,
+                            int32_t *near_ties) {
+    if (!idx && n > 0) return fail(BK_EINVAL, "null batch indices");
+    return roni_softmax_host(c, ww, deltas, n, ld, idx, nb, scores, near_ties);
 }

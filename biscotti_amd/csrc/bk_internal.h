@@ -151,12 +151,24 @@ size_t roni_ws(int64_t n, int64_t d);
 hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, const double *yv,
                        const double *ww, const double *deltas, int64_t n, int64_t ld,
                        double *ws, unsigned int *cnt, double *scores, hipStream_t st);
-// the torch-path (softmax model) RONI, K8: ws = roni_softmax_ws(n, din, nv, C) bytes
+// the torch-path (softmax model) RONI, K8: ws = roni_softmax_ws(n, din, nv, C) bytes;
+// good: 2 (n + 1) counters; xn: the samples' norms (nullable: computed into ws);
+// near_out (nullable): the n + 1 near-tie counts (ww, then each update's model)
 size_t roni_softmax_ws(int64_t n, int64_t din, int64_t nv, int C);
+double roni_softmax_g(int64_t din);
+hipError_t launch_roni_xnorm(const float *Xv, int64_t nv, int64_t din, int64_t ldv, double *xn,
+                             hipStream_t st);
 hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
                                const int32_t *yv, int C, const double *ww, const double *deltas,
-                               int64_t n, int64_t ld, double *ws, unsigned int *good,
-                               double *scores, hipStream_t st);
+                               int64_t n, int64_t ld, double *ws, const double *xn,
+                               unsigned int *good, double *scores, int32_t *near_out,
+                               hipStream_t st);
+// K8 on the last mini-batches (idx: n x 2 x nb sample indices; near_out nullable, 2 n)
+hipError_t launch_roni_softmax_batches(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
+                                       const int32_t *yv, int C, const double *ww,
+                                       const double *deltas, int64_t n, int64_t ld,
+                                       const int64_t *idx, int64_t nb, double *scores,
+                                       int32_t *near_out, hipStream_t st);
 // bk_small.hip: the whole Multi-Krum of a small batch (n <= 128) in one launch
 struct SmallPlan {
     int nb16 = 0, nblk = 0, kc = 0, P = 0, ng = 0, Q = 0, nS = 0, C = 0;  // P chunks, ng G items

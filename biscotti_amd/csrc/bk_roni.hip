@@ -9,21 +9,19 @@
 // batched over n updates: model 0 is ww, model j >= 1 is ww + delta_{j-1}
 // (added elementwise in fp64 first, as numpy does).
 //
-//   K7  k_roni_count   grid (row chunks, groups of 16 models): the block
-//                      builds its 16 models in LDS ([d][16], broadcast reads),
-//                      each thread takes validation rows and runs 16 fp64 dots
-//                      per row from one pass over the row, np.sign semantics
-//                      (0 -> 0, NaN -> NaN), per-model wave sums of the
-//                      mismatches, one integer atomic per wave and model
-//                      (counts are exact and order-free)
+//   K7  k_roni_mm_prep<false> + k_roni_sign   the logistic verifier as one
+//                      fp64-MFMA GEMM (samples x models) with np.sign and the
+//                      mismatch count fused into its epilogue
 //   K7b k_roni_score   score[i] = cnt[i+1]/nv - cnt[0]/nv in fp64
+//   K8  the torch-path (softmax) verifier: k_roni_mm_prep<true> +
+//       k_roni_logits over a whole sample set, or k_roni_batch over the last
+//       mini-batches the reference actually scores (below)
 //
-// Bound: the validation set is re-read once per 16 models (from L2 / Infinity
-// Cache for creditcard-sized sets: 85,000 x 25 fp64 = 17 MB); the dots are
-// fp64 VALU work, 16 independent FMA chains per row.  Built with
-// -ffp-contract=off: ww + delta rounds exactly like numpy; the dot itself is a
-// plain fp64 FMA chain (BLAS order is library-specific: only the sign matters,
-// and it differs from numpy's only for dots within rounding of 0).
+// Built with -ffp-contract=off: ww + delta rounds exactly like numpy; every dot
+// is a plain fp64 FMA chain over k ascending (the MFMA chains round alike,
+// tools/probe_mfma_order.hip).  BLAS order is library-specific: only the sign
+// (K7) or the argmax (K8) matters, and they differ from the reference's only
+// within rounding (K8 counts those samples: "near ties").
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -31,66 +29,6 @@
 #include "bk_internal.h"
 
 namespace bk {
-
-// A/B knob: BK_RONI_VALU=1 runs the r3a VALU kernels (K7 for d <= 1024, K8)
-static bool roni_valu() {
-    static const bool v = [] {
-        const char *e = probe_env("BK_RONI_VALU");
-        return e && atoi(e) != 0;
-    }();
-    return v;
-}
-
-constexpr int RONI_ROWS = 1024;  // validation rows per block (4 per thread)
-constexpr int RONI_MPB = 16;     // models per block: each x element loaded feeds 16 FMAs
-
-// grid (row chunks, model groups); models m0 .. m0+15 of the n+1 (0 = ww)
-__global__ __launch_bounds__(256) void k_roni_count(const double *__restrict__ Xv, int64_t nv,
-                                                    int64_t d, int64_t ldv,
-                                                    const double *__restrict__ yv,
-                                                    const double *__restrict__ ww,
-                                                    const double *__restrict__ deltas, int64_t ld,
-                                                    int64_t nmod, unsigned int *__restrict__ cnt) {
-    extern __shared__ __attribute__((aligned(16))) double w[];  // [d][RONI_MPB]
-    const int64_t m0 = (int64_t)blockIdx.y * RONI_MPB;
-    for (int64_t e = threadIdx.x; e < d * RONI_MPB; e += 256) {
-        const int64_t k = e / RONI_MPB, j = m0 + e % RONI_MPB;
-        double v = 0.0;  // models past the end: never counted
-        if (j < nmod) v = j == 0 ? ww[k] : ww[k] + deltas[(j - 1) * ld + k];
-        w[e] = v;
-    }
-    __syncthreads();
-    unsigned int mine[RONI_MPB];
-#pragma unroll
-    for (int j = 0; j < RONI_MPB; ++j) mine[j] = 0;
-    const int64_t r0 = (int64_t)blockIdx.x * RONI_ROWS;
-    for (int64_t v = r0 + threadIdx.x; v < r0 + RONI_ROWS && v < nv; v += 256) {
-        const double *x = Xv + v * ldv;
-        double s[RONI_MPB];
-#pragma unroll
-        for (int j = 0; j < RONI_MPB; ++j) s[j] = 0.0;
-        for (int64_t k = 0; k < d; ++k) {
-            const double xk = x[k];
-            const double *wk = w + k * RONI_MPB;
-#pragma unroll
-            for (int j = 0; j < RONI_MPB; ++j) s[j] = __builtin_fma(xk, wk[j], s[j]);
-        }
-        const double y = yv[v];
-#pragma unroll
-        for (int j = 0; j < RONI_MPB; ++j) {
-            const double yh = s[j] > 0.0 ? 1.0 : (s[j] < 0.0 ? -1.0 : (s[j] == 0.0 ? 0.0 : s[j]));
-            mine[j] += !(yh == y);  // NaN never equals: an error, as in numpy
-        }
-    }
-    // per model: wave total, then one atomic per wave
-#pragma unroll
-    for (int j = 0; j < RONI_MPB; ++j) {
-        unsigned int tot = mine[j];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
-        if ((threadIdx.x & 63) == 0 && tot && m0 + j < nmod) atomicAdd(&cnt[m0 + j], tot);
-    }
-}
 
 __global__ void k_roni_score(const unsigned int *__restrict__ cnt, int64_t n, int64_t nv,
                              double *__restrict__ scores) {
@@ -100,137 +38,6 @@ __global__ void k_roni_score(const unsigned int *__restrict__ cnt, int64_t n, in
     const double g_err = (double)cnt[0] / dn;
     const double new_err = (double)cnt[i + 1] / dn;
     scores[i] = new_err - g_err;
-}
-
-static hipError_t launch_roni_valu(const double *Xv, int64_t nv, int64_t d, int64_t ldv,
-                                   const double *yv, const double *ww, const double *deltas,
-                                   int64_t n, int64_t ld, unsigned int *cnt, double *scores,
-                                   hipStream_t st) {
-    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)(n + 1) * sizeof(unsigned int), st);
-    if (e != hipSuccess) return e;
-    const dim3 grid((unsigned)((nv + RONI_ROWS - 1) / RONI_ROWS),
-                    (unsigned)((n + 1 + RONI_MPB - 1) / RONI_MPB));
-    hipLaunchKernelGGL(k_roni_count, grid, dim3(256), (size_t)d * RONI_MPB * sizeof(double), st,
-                       Xv, nv, d, ldv, yv, ww, deltas, ld, n + 1, cnt);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_roni_score, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cnt, n,
-                       nv, scores);
-    return hipGetLastError();
-}
-
-
-// ---------------------------------------------------------------------------
-// K8: the torch-path RONI (the mnist / lfw softmax verifiers) --
-// client_obj.roni(ww, delta), ML/Pytorch/client_obj.py:100-112: the flat
-// weights [W (C x D_in, row-major), b (C)] rounded to fp32 after the fp64
-// add (SoftmaxModel.reshape -> torch.FloatTensor, softmax_model.py:19-24), the
-// training error 1 - accuracy of argmax(x W^T + b) (client.py:131-139), and
-// score = err(ww + delta) - err(ww).  d = 7,850 for mnist: the model no longer
-// fits K7's LDS layout, and the error is a 10-way argmax, not a sign.
-//
-//   K8a k_roni_mc_prep   Wm[j][k][c] = fp32(ww + delta_j) widened to fp64,
-//                        classes padded to 16 (one 128-B row per feature, so
-//                        a wave's model row is read with wave-uniform scalar
-//                        loads), bm[j][c] the biases
-//   K8b k_roni_mc_count  grid (64-sample chunks, groups of 4 models): wave w
-//                        runs model 4 y + w, lane l sample 64 x + l.  The
-//                        chunk's samples are staged 64 features at a time in
-//                        LDS, transposed ([k][sample]: a lane's reads are
-//                        consecutive words); each lane runs C fp64 FMA chains
-//                        over k ascending (every fp32 x fp32 product is exact
-//                        in fp64), adds the bias, rounds the logits to fp32,
-//                        takes np.argmax (first maximum; a NaN is the maximum)
-//                        and the wave counts correct predictions (ballot).
-//   K8c k_roni_mc_score  score[i] = (1 - good[i+1]/nv) - (1 - good[0]/nv)
-//
-// Bound: fp64 VALU (nv x (n+1) x C x D_in FMAs); the samples are re-read
-// once per 4 models (L2), the models once per 64 samples (scalar cache).
-constexpr int RMC_S = 64, RMC_M = 4, RMC_KC = 64, RMC_CP = 16;
-
-__global__ __launch_bounds__(256) void k_roni_mc_prep(const double *__restrict__ ww,
-                                                      const double *__restrict__ deltas, int64_t ld,
-                                                      int64_t din, int C, double *__restrict__ Wm,
-                                                      double *__restrict__ bm) {
-    const int64_t j = blockIdx.y;
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // k * 16 + c
-    const int64_t k = e >> 4;
-    const int c = (int)(e & 15);
-    if (k < din) {
-        double v = 0.0;  // padding classes: zero weights, never compared
-        if (c < C) {
-            const int64_t idx = (int64_t)c * din + k;
-            v = (double)(float)(j == 0 ? ww[idx] : ww[idx] + deltas[(j - 1) * ld + idx]);
-        }
-        Wm[(j * din + k) * RMC_CP + c] = v;
-    }
-    if (blockIdx.x == 0 && threadIdx.x < RMC_CP) {
-        const int cc = (int)threadIdx.x;
-        double v = 0.0;
-        if (cc < C) {
-            const int64_t idx = (int64_t)C * din + cc;
-            v = (double)(float)(j == 0 ? ww[idx] : ww[idx] + deltas[(j - 1) * ld + idx]);
-        }
-        bm[j * RMC_CP + cc] = v;
-    }
-}
-
-// NC: classes computed (compile time); C: classes compared (C <= NC)
-template <int NC>
-__global__ __launch_bounds__(256) void k_roni_mc_count(const float *__restrict__ Xv, int64_t nv,
-                                                       int64_t din, int64_t ldv,
-                                                       const int32_t *__restrict__ yv, int C,
-                                                       const double *__restrict__ Wm,
-                                                       const double *__restrict__ bm, int64_t nmod,
-                                                       unsigned int *__restrict__ good) {
-    __shared__ float xs[RMC_KC][RMC_S + 1];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t j = (int64_t)blockIdx.y * RMC_M + wave;
-    const int64_t jj = j < nmod ? j : nmod - 1;  // an idle wave reads a real model, never counts
-    const int64_t s0 = (int64_t)blockIdx.x * RMC_S;
-    const double *wj = Wm + jj * din * RMC_CP;
-    double acc[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
-    // staging: thread t moves features (t & 3) * 16 .. + 15 of sample t >> 2
-    const int ts = tid >> 2, tk = (tid & 3) * 16;
-    const int64_t srow = s0 + ts < nv ? s0 + ts : nv - 1;
-    const float *xrow = Xv + srow * ldv;
-    for (int64_t k0 = 0; k0 < din; k0 += RMC_KC) {
-        __syncthreads();  // the previous chunk has been consumed
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int64_t k = k0 + tk + u;
-            xs[tk + u][ts] = k < din ? xrow[k] : 0.0f;
-        }
-        __syncthreads();
-        const int kn = (int)(din - k0 < RMC_KC ? din - k0 : RMC_KC);
-        const double *wk = wj + k0 * RMC_CP;
-        for (int kk = 0; kk < kn; ++kk) {
-            const double x = (double)xs[kk][lane];
-#pragma unroll
-            for (int c = 0; c < NC; ++c) acc[c] = __builtin_fma(x, wk[kk * RMC_CP + c], acc[c]);
-        }
-    }
-    // logits in fp32, np.argmax: the first maximum, a NaN wins at its first place
-    int best = 0;
-    float bl = 0.0f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        if (c >= C) break;
-        const float lg = (float)(acc[c] + bm[jj * RMC_CP + c]);
-        if (c == 0) {
-            bl = lg;
-        } else if (!(bl != bl) && (lg != lg || lg > bl)) {
-            best = c;
-            bl = lg;
-        }
-    }
-    const int64_t s = s0 + lane;
-    const bool ok = s < nv && best == yv[s < nv ? s : nv - 1];
-    const unsigned int cnt = (unsigned int)__popcll(__ballot(ok));
-    if (lane == 0 && j < nmod && cnt) atomicAdd(&good[j], cnt);
 }
 
 __global__ void k_roni_mc_score(const unsigned int *__restrict__ good, int64_t n, int64_t nv,
@@ -335,6 +142,74 @@ __global__ __launch_bounds__(256) void k_roni_mm_prep(const double *__restrict__
 // LDS tile, then wave w takes models w, w + 4, ... of the tile, lane l sample
 // l: np.argmax over the C logits, one ballot count and one atomic per model
 // and workgroup.
+// K8's near-tie test (oracle/roni_oracle.c softmax_eval, the same fp64
+// expression): the winning logit l1 (class a) and the best other l2 can swap
+// under torch's fp32 sgemm rounding only if
+//     !( l1 - l2 - u (|l1| + |l2|)  >  E_a + max_c E_c ),  E_c = g (|x| |w_c| + |b_c|)
+// (g = gamma_{d_in + 1}(2^-24) (1 + 2^-10), host-computed), or a logit is not
+// finite.  xn = |x| of the sample, wn / b the model's C weight-row norms and
+// biases (fp32 values), all fp64.
+__device__ inline bool softmax_near_tie(const float *lg, int C, int best, double xn,
+                                        const double *wn, const double *b, double g) {
+    double wmax = 0.0, bmax = 0.0, l2 = -__builtin_inf();
+    bool fin = true;
+    for (int c = 0; c < C; ++c) {
+        const double w = wn[c], ab = __builtin_fabs(b[c]), v = (double)lg[c];
+        wmax = w > wmax ? w : wmax;
+        bmax = ab > bmax ? ab : bmax;
+        fin = fin && __builtin_isfinite(v);
+        if (c != best && v > l2) l2 = v;
+    }
+    const double u = 0x1p-24, l1 = (double)lg[best];
+    const double ea = g * (xn * wn[best] + __builtin_fabs(b[best]));
+    const double emax = g * (xn * wmax + bmax);
+    return !fin || !(l1 - l2 - u * (__builtin_fabs(l1) + __builtin_fabs(l2)) > ea + emax);
+}
+
+// |x_s| for every sample: a workgroup stages 64 samples x 64 features through
+// LDS (coalesced), then thread s sums its row's squares in k order -- the
+// oracle's sequential sum, bit for bit (every fp32 square is exact in fp64)
+__global__ __launch_bounds__(256) void k_roni_xnorm(const float *__restrict__ Xv, int64_t nv,
+                                                    int64_t din, int64_t ldv,
+                                                    double *__restrict__ xn) {
+    __shared__ float t[64][65];
+    const int tid = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * 64;
+    double acc = 0.0;
+    for (int64_t k0 = 0; k0 < din; k0 += 64) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int r = (tid >> 6) + 4 * u, kk = tid & 63;
+            const int64_t sr = s0 + r < nv ? s0 + r : nv - 1;
+            t[r][kk] = k0 + kk < din ? Xv[sr * ldv + k0 + kk] : 0.0f;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const int kn = (int)(din - k0 < 64 ? din - k0 : 64);
+            for (int kk = 0; kk < kn; ++kk) {
+                const double v = (double)t[tid][kk];
+                acc += v * v;
+            }
+        }
+    }
+    if (tid < 64 && s0 + tid < nv) xn[s0 + tid] = __builtin_sqrt(acc);
+}
+
+// |w_col| of every model-class column of Wt (the fp32 weights widened), k in
+// order: the oracle's sequential sum.  Coalesced across columns.
+__global__ __launch_bounds__(256) void k_roni_wnorm(const double *__restrict__ Wt, int64_t ldl,
+                                                    int64_t din, double *__restrict__ wn) {
+    const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (col >= ldl) return;
+    double acc = 0.0;
+    for (int64_t k = 0; k < din; ++k) {
+        const double v = Wt[k * ldl + col];
+        acc += v * v;
+    }
+    wn[col] = __builtin_sqrt(acc);
+}
+
 constexpr int RG_MT = 64, RG_NT = 128, RG_LT = RG_NT + 1;
 constexpr int RL_KC = 64, RL_XS = 68;
 
@@ -344,7 +219,10 @@ __global__ __launch_bounds__(256) void k_roni_logits(const float *__restrict__ X
                                                      const double *__restrict__ Wt,
                                                      const double *__restrict__ bt, int64_t ldl,
                                                      int64_t nmod, int nx, int xcd_cols,
-                                                     unsigned int *__restrict__ good) {
+                                                     unsigned int *__restrict__ good,
+                                                     const double *__restrict__ xn,
+                                                     const double *__restrict__ wnrm, double g,
+                                                     unsigned int *__restrict__ near) {
     __shared__ float xs[RG_MT][RL_XS];
     __shared__ float lt[RG_MT][RG_LT];
     const int tid = threadIdx.x, l = tid & 63;
@@ -443,11 +321,14 @@ __global__ __launch_bounds__(256) void k_roni_logits(const float *__restrict__ X
     __syncthreads();
     // np.argmax: the first maximum, a NaN wins at its first place
     const int64_t s = s0 + l;
-    const int ysl = yv[s < nv ? s : nv - 1];
+    const int64_t sc = s < nv ? s : nv - 1;
+    const int ysl = yv[sc];
+    const double xnl = xn[sc];
     for (int p = wave; p < P; p += 4) {
         const int64_t j = (int64_t)ty * P + p;
         if (j >= nmod) break;  // wave-uniform
         const float *lg = &lt[l][p * C];
+        const int64_t col0 = cb + (int64_t)p * C;
         int best = 0;
         float bl = lg[0];
         for (int c = 1; c < C; ++c) {
@@ -457,8 +338,11 @@ __global__ __launch_bounds__(256) void k_roni_logits(const float *__restrict__ X
                 bl = v;
             }
         }
+        const bool nt = softmax_near_tie(lg, C, best, xnl, wnrm + col0, bt + col0, g);
         const unsigned int ok = (unsigned int)__popcll(__ballot(s < nv && best == ysl));
+        const unsigned int nn = (unsigned int)__popcll(__ballot(s < nv && nt));
         if (l == 0 && ok) atomicAdd(&good[j], ok);
+        if (l == 0 && nn) atomicAdd(&near[j], nn);
     }
 }
 
@@ -591,62 +475,199 @@ __global__ __launch_bounds__(256) void k_roni_sign(const double *__restrict__ Xv
     }
 }
 
-size_t roni_softmax_ws(int64_t n, int64_t din, int64_t nv, int C) {
-    (void)nv;
-    const int64_t ldl = rmm_ldl(n, C);
-    const size_t mm = (size_t)(rmm_rows(din) + 1) * ldl * sizeof(double);
-    const size_t mc = (size_t)(n + 1) * ((size_t)din * RMC_CP + RMC_CP) * sizeof(double);
-    return mm > mc ? mm : mc;
+double roni_softmax_g(int64_t din) {
+    const double u = 0x1p-24, nn = (double)(din + 1);
+    return nn * u / (1.0 - nn * u) * (1.0 + 0x1p-10);
 }
 
-static hipError_t launch_roni_softmax_mm(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
-                                         const int32_t *yv, int C, const double *ww,
-                                         const double *deltas, int64_t n, int64_t ld, double *ws,
-                                         unsigned int *good, double *scores, hipStream_t st) {
+// Wt ((rows + 1) x ldl: the weights, then the biases), wn (ldl), xn (nv)
+size_t roni_softmax_ws(int64_t n, int64_t din, int64_t nv, int C) {
+    const int64_t ldl = rmm_ldl(n, C);
+    return ((size_t)(rmm_rows(din) + 1) * ldl + (size_t)ldl + (size_t)nv) * sizeof(double);
+}
+
+hipError_t launch_roni_xnorm(const float *Xv, int64_t nv, int64_t din, int64_t ldv, double *xn,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(k_roni_xnorm, dim3((unsigned)((nv + 63) / 64)), dim3(256), 0, st, Xv, nv, din,
+                       ldv, xn);
+    return hipGetLastError();
+}
+
+// xn: the samples' norms (nullable: computed here into the workspace);
+// good / near: 2 (n + 1) counters (correct predictions, then near ties)
+hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
+                               const int32_t *yv, int C, const double *ww, const double *deltas,
+                               int64_t n, int64_t ld, double *ws, const double *xn,
+                               unsigned int *good, double *scores, int32_t *near_out,
+                               hipStream_t st) {
     const int64_t nmod = n + 1, ldl = rmm_ldl(n, C), rows = rmm_rows(din);
-    double *Wt = ws, *bt = ws + rows * ldl;
-    hipError_t e = hipMemsetAsync(good, 0, (size_t)nmod * sizeof(unsigned int), st);
+    double *Wt = ws, *bt = ws + rows * ldl, *wn = bt + ldl, *xw = wn + ldl;
+    unsigned int *near = good + nmod;
+    hipError_t e = hipMemsetAsync(good, 0, (size_t)2 * nmod * sizeof(unsigned int), st);
     if (e != hipSuccess) return e;
+    if (!xn) {
+        if ((e = launch_roni_xnorm(Xv, nv, din, ldv, xw, st)) != hipSuccess) return e;
+        xn = xw;
+    }
     hipLaunchKernelGGL(k_roni_mm_prep<true>, dim3((unsigned)(ldl / 64), (unsigned)((rows + 31) / 32)),
                        dim3(256), 0, st, ww, deltas, ld, din, C, nmod, ldl, rows, Wt, bt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_roni_wnorm, dim3((unsigned)((ldl + 255) / 256)), dim3(256), 0, st, Wt, ldl,
+                       din, wn);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int64_t nx64 = (nv + RG_MT - 1) / RG_MT, ny64 = ldl / RG_NT;
     if (nx64 * ny64 > 0x7fffffff) return hipErrorInvalidConfiguration;  // grid limit
     const int nx = (int)nx64, ny = (int)ny64;
     hipLaunchKernelGGL(k_roni_logits, dim3((unsigned)(nx * ny)), dim3(256), 0, st, Xv, nv, din, ldv,
-                       yv, C, Wt, bt, ldl, nmod, nx, ny % 8 == 0 ? 1 : 0, good);
+                       yv, C, Wt, bt, ldl, nmod, nx, ny % 8 == 0 ? 1 : 0, good, xn, wn,
+                       roni_softmax_g(din), near);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_roni_mc_score, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, good,
                        n, nv, scores);
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (near_out)
+        e = hipMemcpyAsync(near_out, near, (size_t)nmod * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                           st);
+    return e;
 }
 
-hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
-                               const int32_t *yv, int C, const double *ww, const double *deltas,
-                               int64_t n, int64_t ld, double *ws, unsigned int *good,
-                               double *scores, hipStream_t st) {
-    if (!roni_valu())
-        return launch_roni_softmax_mm(Xv, nv, din, ldv, yv, C, ww, deltas, n, ld, ws, good, scores,
-                                      st);
-    const int64_t nmod = n + 1;
-    double *Wm = ws, *bm = ws + (size_t)nmod * din * RMC_CP;
-    hipError_t e = hipMemsetAsync(good, 0, (size_t)nmod * sizeof(unsigned int), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_roni_mc_prep, dim3((unsigned)((din * RMC_CP + 255) / 256), (unsigned)nmod),
-                       dim3(256), 0, st, ww, deltas, ld, din, C, Wm, bm);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    const dim3 grid((unsigned)((nv + RMC_S - 1) / RMC_S), (unsigned)((nmod + RMC_M - 1) / RMC_M));
-    if (C == 2)
-        hipLaunchKernelGGL(k_roni_mc_count<2>, grid, dim3(256), 0, st, Xv, nv, din, ldv, yv, C, Wm, bm, nmod, good);
-    else if (C == 10)
-        hipLaunchKernelGGL(k_roni_mc_count<10>, grid, dim3(256), 0, st, Xv, nv, din, ldv, yv, C, Wm, bm, nmod, good);
-    else if (C == 12)
-        hipLaunchKernelGGL(k_roni_mc_count<12>, grid, dim3(256), 0, st, Xv, nv, din, ldv, yv, C, Wm, bm, nmod, good);
-    else
-        hipLaunchKernelGGL(k_roni_mc_count<RMC_CP>, grid, dim3(256), 0, st, Xv, nv, din, ldv, yv, C, Wm, bm, nmod, good);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_roni_mc_score, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, good,
-                       n, nv, scores);
+// ---------------------------------------------------------------------------
+// K8 with the reference's batch semantics.  getTrainErr
+// (ML/Pytorch/client.py:136-144) walks the SHUFFLED trainloader (client.py:20)
+// and returns the error of its LAST mini-batch only (the loop overwrites pred
+// and labels): client_obj.roni (client_obj.py:100-112) measures `original`
+// (model ww) and `after` (model ww + delta) on two different random batches of
+// batch_size samples (10 in Biscotti, honest.go:47).  The caller draws them and
+// passes per update j the sample indices idx[(2 j) nb ..] and idx[(2 j + 1) nb ..].
+//
+//   k_roni_batch   one workgroup per update, both evaluations: the two models'
+//                  fp32 weights (ww, and ww + delta_j rounded after the fp64 add)
+//                  and the two batches' samples staged through LDS in chunks of
+//                  RB_KC features; thread (e, s, c) runs logit c of sample s of
+//                  evaluation e as the fp64 FMA chain over k ascending (the
+//                  oracle's, bit for bit), rounds fp32(acc + b); then np.argmax,
+//                  the correct count, the near-tie count (the same test as the
+//                  full-set kernel) and the score, written by the workgroup.
+// Bound: HBM -- each update's delta (C (d_in + 1) fp64) and its 2 nb gathered
+// samples are read once; the FMA work is 2 nb C d_in per update.
+constexpr int RB_ST = 8, RB_KC = 128, RB_KP = RB_KC + 4;
+
+__global__ __launch_bounds__(256) void k_roni_batch(const float *__restrict__ Xv, int64_t nv,
+                                                    int64_t din, int64_t ldv,
+                                                    const int32_t *__restrict__ yv, int C,
+                                                    const double *__restrict__ ww,
+                                                    const double *__restrict__ deltas, int64_t ld,
+                                                    const int64_t *__restrict__ idx, int64_t nb,
+                                                    double g, double *__restrict__ scores,
+                                                    int32_t *__restrict__ near_out) {
+    __shared__ float xs[2][RB_ST][RB_KP];
+    __shared__ float wsm[2][16][RB_KP];
+    __shared__ float lgs[2][RB_ST][16];
+    __shared__ double xnl[2][RB_ST], wnl[2][16], bl[2][16];
+    __shared__ unsigned int cnt[5];  // good0, good1, near0, near1, bad index
+    const int tid = threadIdx.x;
+    const int64_t j = blockIdx.x;
+    const double *dj = deltas + j * ld;
+    const int64_t *ix = idx + 2 * j * nb;
+    const int nlog = 2 * RB_ST * C;
+    const bool lt = tid < nlog;
+    const int le = tid / (RB_ST * C), lr = tid - le * (RB_ST * C), ls = lr / C, lc = lr - ls * C;
+    if (tid < 5) cnt[tid] = 0;
+    if (tid < 2 * C) {  // the two models' fp32 biases
+        const int e = tid / C, c = tid - e * C;
+        const int64_t bi = (int64_t)C * din + c;
+        bl[e][c] = (double)(float)(e == 0 ? ww[bi] : ww[bi] + dj[bi]);
+    }
+    double wnacc = 0.0;  // thread (e, s = 0, c): |w_c| of model e (first tile)
+    unsigned int good[2] = {0, 0}, near[2] = {0, 0};
+    for (int64_t st0 = 0; st0 < nb; st0 += RB_ST) {
+        const int ns = (int)(nb - st0 < RB_ST ? nb - st0 : RB_ST);
+        double acc = 0.0, xacc = 0.0;  // logit (le, ls, lc); thread c == 0: |x_s|
+        for (int64_t k0 = 0; k0 < din; k0 += RB_KC) {
+            const int kn = (int)(din - k0 < RB_KC ? din - k0 : RB_KC);
+            __syncthreads();  // the previous chunk has been consumed
+            for (int i = tid; i < 2 * C * RB_KC; i += 256) {
+                const int e = i / (C * RB_KC), r = i - e * (C * RB_KC), c = r / RB_KC,
+                          kk = r - c * RB_KC;
+                float w = 0.0f;
+                if (kk < kn) {
+                    const int64_t wi = (int64_t)c * din + k0 + kk;
+                    w = (float)(e == 0 ? ww[wi] : ww[wi] + dj[wi]);
+                }
+                wsm[e][c][kk] = w;
+            }
+            for (int i = tid; i < 2 * RB_ST * RB_KC; i += 256) {
+                const int e = i / (RB_ST * RB_KC), r = i - e * (RB_ST * RB_KC), s = r / RB_KC,
+                          kk = r - s * RB_KC;
+                const int ss = s < ns ? s : 0;  // padding rows repeat sample 0 (never counted)
+                int64_t row = ix[e * nb + st0 + ss];
+                if (row < 0 || row >= nv) {
+                    cnt[4] = 1;  // reported as score NaN, near ties -1; never read out of range
+                    row = 0;
+                }
+                xs[e][s][kk] = kk < kn ? Xv[row * ldv + k0 + kk] : 0.0f;
+            }
+            __syncthreads();
+            if (lt) {
+                const float *xr = xs[le][ls], *wr = wsm[le][lc];
+                for (int kk = 0; kk < kn; ++kk) {
+                    const double x = (double)xr[kk];
+                    acc = __builtin_fma(x, (double)wr[kk], acc);
+                    if (lc == 0) xacc += x * x;
+                    if (ls == 0 && st0 == 0) wnacc += (double)wr[kk] * (double)wr[kk];
+                }
+            }
+        }
+        if (lt) {
+            lgs[le][ls][lc] = (float)(acc + bl[le][lc]);
+            if (lc == 0) xnl[le][ls] = __builtin_sqrt(xacc);
+            if (ls == 0 && st0 == 0) wnl[le][lc] = __builtin_sqrt(wnacc);
+        }
+        __syncthreads();
+        if (tid < 2 * RB_ST) {
+            const int e = tid / RB_ST, s = tid - e * RB_ST;
+            if (s < ns) {
+                const float *lg = lgs[e][s];
+                int best = 0;
+                float b0 = lg[0];
+                for (int c = 1; c < C; ++c)
+                    if (!(b0 != b0) && (lg[c] != lg[c] || lg[c] > b0)) {
+                        best = c;
+                        b0 = lg[c];
+                    }
+                int64_t row = ix[e * nb + st0 + s];
+                row = row < 0 || row >= nv ? 0 : row;
+                good[e] += best == yv[row];
+                near[e] += softmax_near_tie(lg, C, best, xnl[e][s], wnl[e], bl[e], g);
+            }
+        }
+    }
+    if (tid < 2 * RB_ST) {
+        atomicAdd(&cnt[0], good[0]);
+        atomicAdd(&cnt[1], good[1]);
+        atomicAdd(&cnt[2], near[0]);
+        atomicAdd(&cnt[3], near[1]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const double dn = (double)nb;
+        const double orig = 1.0 - (double)cnt[0] / dn, after = 1.0 - (double)cnt[1] / dn;
+        const bool bad = cnt[4] != 0;
+        scores[j] = bad ? __builtin_nan("") : after - orig;
+        if (near_out) {
+            near_out[2 * j] = bad ? -1 : (int32_t)cnt[2];
+            near_out[2 * j + 1] = bad ? -1 : (int32_t)cnt[3];
+        }
+    }
+}
+
+hipError_t launch_roni_softmax_batches(const float *Xv, int64_t nv, int64_t din, int64_t ldv,
+                                       const int32_t *yv, int C, const double *ww,
+                                       const double *deltas, int64_t n, int64_t ld,
+                                       const int64_t *idx, int64_t nb, double *scores,
+                                       int32_t *near_out, hipStream_t st) {
+    hipLaunchKernelGGL(k_roni_batch, dim3((unsigned)n), dim3(256), 0, st, Xv, nv, din, ldv, yv, C,
+                       ww, deltas, ld, idx, nb, roni_softmax_g(din), scores, near_out);
     return hipGetLastError();
 }
 
@@ -664,8 +685,6 @@ size_t roni_ws(int64_t n, int64_t d) {
 hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, const double *yv,
                        const double *ww, const double *deltas, int64_t n, int64_t ld,
                        double *ws, unsigned int *cnt, double *scores, hipStream_t st) {
-    if (roni_valu() && d <= 1024)
-        return launch_roni_valu(Xv, nv, d, ldv, yv, ww, deltas, n, ld, cnt, scores, st);
     const int64_t nmod = n + 1, ldl = (nmod + RMM_NT - 1) / RMM_NT * RMM_NT, rows = rmm_rows(d);
     hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nmod * sizeof(unsigned int), st);
     if (e != hipSuccess) return e;

@@ -68,13 +68,25 @@ class RONIValidator:
 
 class SoftmaxRONIValidator(RONIValidator):
     """The torch-path verifier (ML/Pytorch/client_obj.py:100-112: the mnist /
-    lfw softmax models): err = 1 - accuracy of argmax(x W^T + b) over the
-    validation samples (client.py:131-139), the flat weights [W (C x d_in),
-    b (C)] rounded to fp32 as SoftmaxModel.reshape does.  One validation set
-    resident on one GPU (bk_roni_softmax_set_validation)."""
+    lfw softmax models): err = 1 - accuracy of argmax(x W^T + b)
+    (client.py:136-144), the flat weights [W (C x d_in), b (C)] rounded to fp32
+    as SoftmaxModel.reshape does.  The client's training shard is resident on
+    one GPU (bk_roni_softmax_set_validation).
+
+    Which samples: getTrainErr walks the SHUFFLED trainloader (client.py:20)
+    and returns the error of its LAST mini-batch, so `original` and `after`
+    are each measured on a fresh random last batch of batch_size samples (10
+    in Biscotti, DistSys/honest.go:47).  This mirror draws those batches as the
+    DataLoader does -- a permutation per pass, the last batch its tail of
+    nv % batch_size (or batch_size) samples -- from its own seeded generator,
+    and scores them with bk_roni_softmax_batches.  batch_size=None (or >= nv)
+    scores every evaluation over the whole set (bk_roni_softmax).
+
+    After each call, last_near_ties holds the per-evaluation near-tie counts
+    (bk.h: where torch's fp32 argmax may differ from this one)."""
 
     def __init__(self, Xvalid, yvalid, n_classes, engine: Optional[Engine] = None,
-                 priv_prob: float = 0.0):
+                 priv_prob: float = 0.0, batch_size: Optional[int] = 10, seed=None):
         self._engine = engine if engine is not None else default_engine(0)
         X = np.ascontiguousarray(Xvalid, dtype=np.float32)
         y = np.ascontiguousarray(yvalid, dtype=np.int32)
@@ -84,18 +96,47 @@ class SoftmaxRONIValidator(RONIValidator):
         self.n_classes = int(n_classes)
         self.d = self.n_classes * (self.d_in + 1)
         self.priv_prob = priv_prob
+        self.batch_size = None if batch_size is None or batch_size >= self.nv else int(batch_size)
+        if self.batch_size is not None and self.batch_size < 1:
+            raise ValueError("batch_size must be >= 1")
+        self._rng = np.random.default_rng(seed)
+        self.last_near_ties = None
         check(lib().bk_roni_softmax_set_validation(self._engine.ctx, X.ctypes.data, self.nv,
                                                    self.d_in, self.d_in, y.ctypes.data,
                                                    self.n_classes))
 
-    def scores(self, ww, deltas) -> np.ndarray:
+    def last_batch(self) -> np.ndarray:
+        """One shuffled pass's last mini-batch (DataLoader(shuffle=True))."""
+        perm = self._rng.permutation(self.nv)
+        nb = self.nv % self.batch_size or self.batch_size
+        return perm[self.nv - nb:]
+
+    def draw_batches(self, n) -> np.ndarray:
+        """(n, 2, nb) indices: per update, the batch `original` then the batch
+        `after` is scored on, in the reference's call order."""
+        return np.array([[self.last_batch(), self.last_batch()] for _ in range(n)], dtype=np.int64)
+
+    def scores(self, ww, deltas, idx=None) -> np.ndarray:
         ww = np.ascontiguousarray(ww, dtype=np.float64)
         D = np.ascontiguousarray(np.atleast_2d(deltas), dtype=np.float64)
         if ww.shape != (self.d,) or D.shape[1] != self.d:
             raise ValueError("ww must be (d,) and deltas (n, d) with d = %d" % self.d)
-        out = np.empty(D.shape[0], dtype=np.float64)
-        check(lib().bk_roni_softmax(self._engine.ctx, ww.ctypes.data, D.ctypes.data, D.shape[0],
-                                    self.d, out.ctypes.data))
+        n = D.shape[0]
+        out = np.empty(n, dtype=np.float64)
+        if idx is None and self.batch_size is None:
+            nt = np.empty(n + 1, dtype=np.int32)
+            check(lib().bk_roni_softmax(self._engine.ctx, ww.ctypes.data, D.ctypes.data, n,
+                                        self.d, out.ctypes.data, nt.ctypes.data))
+            self.last_near_ties = nt
+            return out
+        idx = self.draw_batches(n) if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        if idx.ndim != 3 or idx.shape[:2] != (n, 2):
+            raise ValueError("idx must be (n, 2, nb)")
+        nt = np.empty((n, 2), dtype=np.int32)
+        check(lib().bk_roni_softmax_batches(self._engine.ctx, ww.ctypes.data, D.ctypes.data, n,
+                                            self.d, idx.ctypes.data, idx.shape[2],
+                                            out.ctypes.data, nt.ctypes.data))
+        self.last_near_ties = nt
         return out
 
 

@@ -339,27 +339,63 @@ int bk_roni(bk_ctx *ctx, const double *ww, const double *deltas, int64_t n, int6
             double *scores);
 
 /* The torch-path RONI verifier (the mnist / lfw softmax models) --
- * client_obj.roni(ww, delta), ML/Pytorch/client_obj.py:100-112, batched over
- * n updates:
- *     score[i] = err(ww + delta_i) - err(ww),
- *     err(w)   = 1 - mean(argmax_c(x W^T + b) == y)   over the validation set
- * with w = [W (n_classes x d_in, row-major), b (n_classes)] (SoftmaxModel,
- * ML/Pytorch/softmax_model.py:19-24; d = n_classes * (d_in + 1): mnist
- * 10 x 785 = 7,850) rounded to fp32 after the fp64 add (torch.FloatTensor),
- * each logit the fp64 sum over k ascending of the exact fp32 products plus the
- * bias, rounded once to fp32; argmax as numpy's (first maximum, NaN wins).
- * Xv is nv x d_in fp32 (row stride ldv), yv the nv labels (int32).
- * 2 <= n_classes <= 16. */
+ * client_obj.roni(ww, delta), ML/Pytorch/client_obj.py:100-112:
+ *     updateModel(ww);         original = getTrainErr()
+ *     updateModel(ww + delta); after    = getTrainErr();   score = after - original
+ * err(w) = 1 - mean(argmax_c(x W^T + b) == y), with w = [W (n_classes x d_in,
+ * row-major), b (n_classes)] (SoftmaxModel, ML/Pytorch/softmax_model.py:7-24;
+ * d = n_classes * (d_in + 1): mnist 10 x 785 = 7,850) rounded to fp32 after
+ * the fp64 add (torch.FloatTensor), each logit the fp64 sum over k ascending of
+ * the exact fp32 products plus the bias, rounded once to fp32; argmax as
+ * numpy's (first maximum, NaN wins).  Xv is nv x d_in fp32 (row stride ldv),
+ * yv the nv labels (int32).  2 <= n_classes <= 16.
+ *
+ * WHICH SAMPLES: getTrainErr (ML/Pytorch/client.py:136-144) walks the client's
+ * SHUFFLED trainloader (client.py:20, shuffle=True) and returns the error of
+ * the LAST mini-batch only (its loop overwrites pred / labels), so the
+ * reference scores `original` and `after` on two different random batches of
+ * batch_size samples (10 in Biscotti, DistSys/honest.go:47).
+ *   bk_roni_softmax_batches*  that semantics: the caller draws the batches (its
+ *                             loader's shuffles) and passes, per update j, the
+ *                             sample indices idx[(2 j) nb .. + nb) (original,
+ *                             model ww) and idx[(2 j + 1) nb ..] (after, model
+ *                             ww + delta_j); errors are over nb samples
+ *   bk_roni_softmax*          every evaluation over the whole set: the
+ *                             reference with batch_size >= nv (one batch)
+ *
+ * NEAR TIES: torch's CPU sgemm accumulates the logits in fp32 in its own
+ * order, so its argmax can differ from this one only on samples whose top two
+ * logits lie within that rounding.  near_ties (nullable) receives, per
+ * evaluation, the number of samples for which
+ *     !( l1 - l2 - u (|l1| + |l2|) > E_a + max_c E_c ),  E_c = g (|x| |w_c| + |b_c|),
+ * u = 2^-24, g = gamma_{d_in+1}(u) (1 + 2^-10), or any logit is not finite
+ * (l1: the winning logit, class a; l2: the best other).  A score can differ
+ * from the reference's only if one of its two evaluations has a near tie, and
+ * then by at most (near ties) / (samples).  Layout: bk_roni_softmax* n + 1
+ * counts (ww, then each update's model); bk_roni_softmax_batches* 2 n (update
+ * j: original, after).  A device-side batch index outside [0, nv) gives that
+ * update score NaN and near ties -1 (nothing is read out of range); the host
+ * form rejects it with BK_EINVAL. */
 int bk_roni_softmax_device(bk_ctx *ctx, const float *d_Xv, int64_t nv, int64_t d_in, int64_t ldv,
                            const int32_t *d_yv, int64_t n_classes, const double *d_ww,
-                           const double *d_deltas, int64_t n, int64_t ld, double *d_scores);
+                           const double *d_deltas, int64_t n, int64_t ld, double *d_scores,
+                           int32_t *d_near_ties);
+int bk_roni_softmax_batches_device(bk_ctx *ctx, const float *d_Xv, int64_t nv, int64_t d_in,
+                                   int64_t ldv, const int32_t *d_yv, int64_t n_classes,
+                                   const double *d_ww, const double *d_deltas, int64_t n,
+                                   int64_t ld, const int64_t *d_idx, int64_t nb, double *d_scores,
+                                   int32_t *d_near_ties);
 /* The Go verifier's shape (verifyUpdate, honest.go:598-629, bound to the
- * torch module's roni): the validation set once per context, then host
- * updates scored against the chain's latest model; synchronous. */
+ * torch module's roni): the validation set (the client's training shard) once
+ * per context, then host updates scored against the chain's latest model;
+ * synchronous. */
 int bk_roni_softmax_set_validation(bk_ctx *ctx, const float *Xv, int64_t nv, int64_t d_in,
                                    int64_t ldv, const int32_t *yv, int64_t n_classes);
 int bk_roni_softmax(bk_ctx *ctx, const double *ww, const double *deltas, int64_t n, int64_t ld,
-                    double *scores);
+                    double *scores, int32_t *near_ties);
+int bk_roni_softmax_batches(bk_ctx *ctx, const double *ww, const double *deltas, int64_t n,
+                            int64_t ld, const int64_t *idx, int64_t nb, double *scores,
+                            int32_t *near_ties);
 
 /* ---- measurement: per-kernel HIP-event timing on the context stream ------- */
 enum bk_kernel_id {

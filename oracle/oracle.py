@@ -58,8 +58,11 @@ def lib():
         L.oracle_roni.argtypes = [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _vp]
         L.oracle_roni.restype = ctypes.c_int
         L.oracle_roni_softmax.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64,
-                                           _i64, _vp]
+                                           _i64, _vp, _vp]
         L.oracle_roni_softmax.restype = ctypes.c_int
+        L.oracle_roni_softmax_batches.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp,
+                                                   _i64, _i64, _vp, _i64, _vp, _vp]
+        L.oracle_roni_softmax_batches.restype = ctypes.c_int
         L.oracle_go_f64_to_i64.argtypes = [ctypes.c_double]
         L.oracle_go_f64_to_i64.restype = _i64
         L.oracle_num_threads.restype = ctypes.c_int
@@ -225,10 +228,13 @@ def roni(Xv, yv, ww, deltas):
     return out
 
 
-def roni_softmax(Xv, yv, n_classes, ww, deltas):
+def roni_softmax(Xv, yv, n_classes, ww, deltas, near_ties=False):
     """ML/Pytorch/client_obj.py:100-112 (softmax model, getTrainErr) for each
-    row of deltas: scores (n,).  Xv (nv, d_in) float32, yv (nv,) int labels, ww
-    and deltas fp64 of length n_classes * (d_in + 1) ([W row-major, b])."""
+    row of deltas, every update scored on the same sample set (the reference
+    with batch_size >= nv): scores (n,).  Xv (nv, d_in) float32, yv (nv,) int
+    labels, ww and deltas fp64 of length n_classes * (d_in + 1) ([W row-major,
+    b]).  near_ties=True also returns the (n + 1,) near-tie counts (ww, then
+    each update's model)."""
     Xv = np.ascontiguousarray(Xv, dtype=np.float32)
     yv = np.ascontiguousarray(yv, dtype=np.int32)
     ww = np.ascontiguousarray(ww, dtype=np.float64)
@@ -236,6 +242,29 @@ def roni_softmax(Xv, yv, n_classes, ww, deltas):
     nv, din = Xv.shape
     assert ww.shape == (n_classes * (din + 1),) and D.shape[1] == ww.shape[0]
     out = np.empty(D.shape[0], dtype=np.float64)
+    nt = np.empty(D.shape[0] + 1, dtype=np.int32)
     assert lib().oracle_roni_softmax(_ptr(Xv), nv, din, din, _ptr(yv), int(n_classes), _ptr(ww),
-                                     _ptr(D), D.shape[0], D.shape[1], _ptr(out)) == 0
-    return out
+                                     _ptr(D), D.shape[0], D.shape[1], _ptr(out), _ptr(nt)) == 0
+    return (out, nt) if near_ties else out
+
+
+def roni_softmax_batches(Xv, yv, n_classes, ww, deltas, idx):
+    """The reference's last-batch semantics (client.py:136-144): update j's
+    `original` on the samples idx[j, 0] (model ww) and its `after` on idx[j, 1]
+    (model ww + delta_j).  idx (n, 2, nb) int64.  Returns (scores (n,),
+    near_ties (n, 2))."""
+    Xv = np.ascontiguousarray(Xv, dtype=np.float32)
+    yv = np.ascontiguousarray(yv, dtype=np.int32)
+    ww = np.ascontiguousarray(ww, dtype=np.float64)
+    D = np.ascontiguousarray(np.atleast_2d(deltas), dtype=np.float64)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    nv, din = Xv.shape
+    n = D.shape[0]
+    assert idx.ndim == 3 and idx.shape[:2] == (n, 2)
+    nb = idx.shape[2]
+    out = np.empty(n, dtype=np.float64)
+    nt = np.empty((n, 2), dtype=np.int32)
+    assert lib().oracle_roni_softmax_batches(_ptr(Xv), nv, din, din, _ptr(yv), int(n_classes),
+                                             _ptr(ww), _ptr(D), n, D.shape[1], _ptr(idx), nb,
+                                             _ptr(out), _ptr(nt)) == 0
+    return out, nt

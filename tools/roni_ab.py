@@ -1,6 +1,6 @@
 """A/B of the RONI kernels (K7 logistic, K8 softmax) at bench.py's shapes, in
 one process per mode: run as  python tools/roni_ab.py  (MFMA, the default) and
-BK_RONI_VALU=1 python tools/roni_ab.py  (the r3a VALU kernels).  Prints one
+LIB=<another build> python tools/roni_ab.py  (an A/B build).  Prints one
 JSON line with the kernel times and a hash of the score bits, so two modes can
 be compared bit for bit."""
 import hashlib
@@ -22,7 +22,7 @@ def main():
     eng = Engine(0)
     dev = torch.device("cuda:0")
     g2 = torch.Generator(device=dev).manual_seed(5)
-    out = {"mode": "valu" if os.environ.get("BK_RONI_VALU", "0") != "0" else "mfma"}
+    out = {"lib": _lib.LIB_PATH}
     nv, dr, nr = 85_000, 25, 512
     Xv = torch.randn((nv, dr), dtype=torch.float64, device=dev, generator=g2)
     yv = torch.where(torch.randn(nv, dtype=torch.float64, device=dev, generator=g2) > 0, 1.0, -1.0)
@@ -42,7 +42,7 @@ def main():
                    2.0 * nv * (nr + 1) * dr),
         "k_roni_softmax": (lambda: check(lib().bk_roni_softmax_device(
             eng.ctx, Xm.data_ptr(), nvm, dinm, dinm, ym.data_ptr(), cm, wm.data_ptr(),
-            dm.data_ptr(), nrm, cm * (dinm + 1), rsm.data_ptr())), rsm,
+            dm.data_ptr(), nrm, cm * (dinm + 1), rsm.data_ptr(), None)), rsm,
             2.0 * nvm * (nrm + 1) * cm * dinm),
     }
     for name, (fn, res, fl) in runs.items():
