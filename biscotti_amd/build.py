@@ -17,7 +17,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
 SOURCES = ["bk_kernels.hip", "bk_small.hip", "bk_aggregate.hip", "bk_roni.hip", "bk_plan.hip",
-           "bk_api.hip"]
+           "bk_i8.hip", "bk_api.hip"]
 FLAGS = [
     "--offload-arch=gfx950",
     "-O3",

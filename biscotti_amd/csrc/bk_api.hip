@@ -61,7 +61,7 @@ const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_transpo
                                             "k_rank",    "k_compact", "k_mean",   "allreduce",
                                             "k_synth",   "h2d",       "d2h",
                                             "k_aggregate", "k_qsum",  "k_noise",
-                                            "k_roni", "k_small"};
+                                            "k_roni", "k_small", "k_slice"};
 
 struct DevBuf {
     void *p = nullptr;
@@ -145,6 +145,14 @@ struct bk_ctx {
         Plan3 p;
     };
     std::vector<CachedPlan> plans;
+    // K1i8 (BK_F32_I8): layouts and device tables per (n, d), and the workspace
+    struct I8Cached {
+        int64_t n = 0, d = 0;
+        I8Layout L;
+        void *tables = nullptr;
+    };
+    std::vector<I8Cached> i8;
+    DevBuf i8ws;
     int gram_variant = 3;  // 3: LDS-shared v3 for aligned fp64; 1: v1 everywhere (BK_GRAM=v1)
     int gram_mode = 0;     // BK_GRAM_MODE: timing-only ablations of v3 (tools/, never tests)
     int f32_mode = BK_F32_EXACT;  // fp32 rows: widened onto the fp64 MFMA, or the fp32 MFMA
@@ -213,7 +221,7 @@ void bind_epoch(bk_ctx *c) {
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                       &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
                       &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws,
-                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt};
+                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -371,9 +379,53 @@ bool f32_mfma_now(const bk_ctx *c, int dtype) {
            (c->f32_mode == BK_F32_MFMA || c->f32_mode == BK_F32_CERTIFIED);
 }
 
+// fp32 rows on the int8-sliced Gram (K1i8) for this call: BK_F32_I8, or
+// BK_F32_I8_CERTIFIED outside its exact re-run; 16-B aligned rows, d >= 64
+bool i8_now(const bk_ctx *c, const void *dX, int dtype, int64_t d, int64_t ld) {
+    return dtype == BK_F32 && !c->force_exact && d >= 64 && (ld % 4) == 0 &&
+           ((uintptr_t)dX % 16) == 0 &&
+           (c->f32_mode == BK_F32_I8 || c->f32_mode == BK_F32_I8_CERTIFIED);
+}
+
+// K1i8's layout (ranges, tile order) and its device tables, cached per (n, d)
+int get_i8(bk_ctx *c, int64_t n, int64_t d, bk_ctx::I8Cached **out) {
+    for (auto &e : c->i8)
+        if (e.n == n && e.d == d) {
+            *out = &e;
+            return BK_OK;
+        }
+    bk_ctx::I8Cached e;
+    e.n = n;
+    e.d = d;
+    e.L = i8_layout((int)n, d);
+    const size_t tb = (size_t)(e.L.R + 1) * 8 + e.L.order.size() * sizeof(int);
+    std::vector<char> h(tb);
+    memcpy(h.data(), e.L.rb.data(), (size_t)(e.L.R + 1) * 8);
+    memcpy(h.data() + (size_t)(e.L.R + 1) * 8, e.L.order.data(), e.L.order.size() * sizeof(int));
+    hipError_t er = hipMalloc(&e.tables, tb);
+    if (er == hipSuccess) er = hipMemcpy(e.tables, h.data(), tb, hipMemcpyHostToDevice);
+    if (er != hipSuccess) {
+        if (e.tables) (void)hipFree(e.tables);
+        return fail(BK_ENOMEM, "K1i8 tables: %s", hipGetErrorString(er));
+    }
+    if (c->i8.size() >= 4) {
+        (void)hipFree(c->i8.front().tables);
+        c->i8.erase(c->i8.begin());
+        ++c->ws_epoch;  // a captured graph may point at the evicted tables
+    }
+    c->i8.push_back(e);
+    *out = &c->i8.back();
+    return BK_OK;
+}
+
 // Everything stage_gram allocates (K1's plan tables and split-K slabs), so a
 // caller can learn of an allocation failure before it launches anything
 int prepare_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld) {
+    if (i8_now(c, dX, dtype, d, ld)) {
+        bk_ctx::I8Cached *e = nullptr;
+        CHK(get_i8(c, n, d, &e));
+        return ensure(c->i8ws, i8_workspace(e->L));
+    }
     if (use_v3(c, dX, dtype, ld)) {
         Plan3 *p3 = nullptr;
         CHK(get_plan3(c, n, d, v3_bk(dtype), &p3));
@@ -389,7 +441,8 @@ int prepare_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int
 // the margin readers)
 int poison_upper(bk_ctx *c, double *U, int64_t n) {
     const int64_t T = (n + 63) / 64;
-    HIPCHK(hipMemsetAsync(U + T * (T + 1) / 2 * 4096, 0xFF, 2 * sizeof(double), c->stream));
+    HIPCHK(hipMemsetAsync(U + T * (T + 1) / 2 * 4096, 0xFF, BK_UPPER_TRAIL * sizeof(double),
+                          c->stream));
     return BK_OK;
 }
 
@@ -397,6 +450,25 @@ int poison_upper(bk_ctx *c, double *U, int64_t n) {
 // then the trailing pair {column count, columns on the fp32 MFMA}, bk_upper_elems)
 int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
                double *U, Plan &pl) {
+    if (i8_now(c, dX, dtype, d, ld)) {
+        // K1i8: digit slices + bound (k_slice), the int8 GEMM (k_gram), the
+        // fixed-order sum of the range partials + the record (k_reduce)
+        bk_ctx::I8Cached *e = nullptr;
+        CHK(get_i8(c, n, d, &e));
+        CHK(ensure(c->i8ws, i8_workspace(e->L)));
+        pl.n = (int)n;
+        pl.d = d;
+        pl.T = (int)((n + 63) / 64);
+        pl.ntile = pl.T * (pl.T + 1) / 2;
+        const I8Layout &L = e->L;
+        void *ws = c->i8ws.p, *tb = e->tables;
+        CHK(timed(c, BK_K_SLICE, [&] {
+            return launch_i8_slice((const float *)dX, ld, (int)n, d, L, ws, tb, c->stream);
+        }));
+        CHK(timed(c, BK_K_GRAM, [&] { return launch_i8_gemm((int)n, L, ws, tb, c->stream); }));
+        CHK(timed(c, BK_K_REDUCE, [&] { return launch_i8_reduce(d, L, ws, U, c->stream); }));
+        return BK_OK;
+    }
     if (use_v3(c, dX, dtype, ld)) {
         Plan3 *p3 = nullptr;
         CHK(get_plan3(c, n, d, v3_bk(dtype), &p3));
@@ -476,8 +548,9 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     double *diag = (double *)c->diag.p, *bnd = (double *)c->bnd.p;
     const int64_t m = n - f;
     const int64_t k = n - f - 2 > 0 ? n - f - 2 : 0;
-    // the packed upper's trailing pair {column count, columns on the fp32 MFMA}:
-    // the margin's d and unit roundoff, totals after an exchange
+    // the packed upper's trailing record {column count, columns on the fp32
+    // MFMA, int8 error bound, 0}: the margin's d, unit roundoff and absolute
+    // Gram error, totals after an exchange
     const double *dcols = U + (size_t)pl.ntile * 4096;
     const double *Ut = nullptr, *dg = nullptr;
     if (scores_transposed((int)n)) {
@@ -935,7 +1008,7 @@ struct DeviceGuard {
 };
 
 bool certified(const bk_ctx *c, int dtype) {
-    return dtype == BK_F32 && c->f32_mode == BK_F32_CERTIFIED;
+    return dtype == BK_F32 && (c->f32_mode == BK_F32_CERTIFIED || c->f32_mode == BK_F32_I8_CERTIFIED);
 }
 
 // BK_F32_CERTIFIED: run on the fp32 MFMA; if the selection margin does not
@@ -983,8 +1056,9 @@ const char *bk_kernel_name(int kid) {
 
 int64_t bk_upper_elems(int64_t n) {
     const int64_t T = (n + 63) / 64;
-    // + the trailing pair {column count, columns on the fp32 MFMA} (K3b's margin)
-    return T * (T + 1) / 2 * 4096 + 2;
+    // + the trailing record {column count, columns on the fp32 MFMA, the int8
+    // Gram's absolute error bound, 0} (K3b's margin; summed by every exchange)
+    return T * (T + 1) / 2 * 4096 + BK_UPPER_TRAIL;
 }
 
 int bk_create(bk_ctx **out, int device) {
@@ -1028,6 +1102,7 @@ int bk_create(bk_ctx **out, int device) {
     if (const char *v = getenv("BK_TEST_FAIL_BEFORE_EXCHANGE")) c->test_fail_exchange = atoi(v);
     e = configure_kernels();
     if (e == hipSuccess) e = configure_aggregate_kernels();
+    if (e == hipSuccess) e = configure_i8_kernels();
     if (e != hipSuccess) {
         (void)hipStreamDestroy(c->own);
         delete c;
@@ -1048,7 +1123,7 @@ void bk_destroy(bk_ctx *c) {
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                           &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
                           &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws,
-                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt};
+                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws};
         if (c->hmargin) (void)hipHostFree(c->hmargin);
         if (c->hout) (void)hipHostFree(c->hout);
         if (c->copy) (void)hipStreamSynchronize(c->copy);
@@ -1064,6 +1139,8 @@ void bk_destroy(bk_ctx *c) {
         }
         for (hipEvent_t ev : c->pool) (void)hipEventDestroy(ev);
         for (auto &cp : c->plans) free_plan(cp.p);
+        for (auto &e : c->i8)
+            if (e.tables) (void)hipFree(e.tables);
         for (auto &cg : c->graphs) drop_graph(cg);
         if (c->comm) (void)ncclCommDestroy(c->comm);
         if (c->own) (void)hipStreamDestroy(c->own);
@@ -1224,7 +1301,7 @@ int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t
 
 int bk_set_f32_mode(bk_ctx *c, int mode) {
     if (!c) return fail(BK_EINVAL, "null context");
-    if (mode != BK_F32_EXACT && mode != BK_F32_MFMA && mode != BK_F32_CERTIFIED)
+    if (mode < BK_F32_EXACT || mode > BK_F32_I8_CERTIFIED)
         return fail(BK_EINVAL, "bad f32 mode %d", mode);
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f32_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in

@@ -124,15 +124,22 @@ __device__ __forceinline__ double gamma_n(double nn, double u) {
 
 // The selection margin record (include/bk.h bk_selection_margin; k_compact):
 // from the boundary scores lo (rank m-1) and hi (rank m), M = max finite
-// G_ii, the Gram's column count d and unit roundoff u_gram, and k.
+// G_ii, the Gram's column count d and unit roundoff u_gram, an absolute bound
+// eg on every Gram element's error beyond that (the int8-sliced Gram, K1i8;
+// 0 otherwise), and k.  A score sums k distances G_ii + G_jj - 2 G_ij, so a
+// Gram error of eg moves each by <= 4 eg:
+//   e = 4 k (M' (gamma_{d+2}(u_G) + 2 u + gamma_k(u)) + eg (1 + gamma_k(u))),
+//   M' = (M + eg) (1 + 2 gamma_{d+2}(u_G))
 //   margin[0..7] = {gap, err_bound, near_tie, M, s_lo, s_hi, d, k}, margin[8] = u_G
+// (u_G is what the certified re-run reads: an int8 record reports 2^-30, so
+// any Gram that is not exact fp64 re-runs on a near tie)
 __device__ __forceinline__ void write_margin(double *margin, double lo, double hi, double M,
-                                             double dg, int64_t k, double u_gram) {
+                                             double dg, int64_t k, double u_gram, double eg = 0.0) {
     const double u = 0x1p-53, kk = (double)k;
     const double gG = gamma_n(dg + 2.0, u_gram), gR = gamma_n(dg + 2.0, u);
     const double gk = gamma_n(kk, u);
-    const double Mt = M * (1.0 + 2.0 * gG);
-    const double e_here = 4.0 * kk * Mt * (gG + 2.0 * u + gk);
+    const double Mt = (M + eg) * (1.0 + 2.0 * gG);
+    const double e_here = 4.0 * kk * (Mt * (gG + 2.0 * u + gk) + eg * (1.0 + gk));
     const double e_ref = 4.0 * kk * Mt * (gR + 2.0 * u + gk);
     const double bound = 2.0 * (e_here + e_ref) * (1.0 + 0x1p-40);
     // NaN scores rank last here and in numpy: a finite-to-NaN boundary is certain
@@ -145,19 +152,21 @@ __device__ __forceinline__ void write_margin(double *margin, double lo, double h
     margin[5] = hi;
     margin[6] = dg;
     margin[7] = kk;
-    margin[8] = u_gram;  // internal (not in the public 8-double record): the re-run decision
+    margin[8] = eg != 0.0 && u_gram < 0x1p-30 ? 0x1p-30 : u_gram;  // internal: the re-run decision
 }
 
 
-// The margin from a packed record's trailing pair {dg, d32}: dg = the Gram's
-// column count, d32 = how many of them were accumulated on the fp32 MFMA
-// (both summed by every exchange).  u_G = 2^-24 as soon as one column was.
+// The margin from a packed record's trailing record {dg, d32, eg}: dg = the
+// Gram's column count, d32 = how many of them were accumulated on the fp32
+// MFMA, eg = the int8-sliced columns' absolute error bound (all summed by every
+// exchange).  u_G = 2^-24 as soon as one column was on the fp32 MFMA.
 //   dg NaN (a rank poisoned its partial: bk_multikrum_sharded_device) -> the
 //          record is invalid (MARGIN_POISONED)
 //   dg < 1 (a caller's record without a column count, e.g. pack_upper(G, 0))
 //          -> the bound is unknown: err_bound = +inf, near_tie = 1
+//   eg +inf (a non-finite input on the int8 path) -> near_tie = 1
 __device__ __forceinline__ void write_margin_rec(double *margin, double lo, double hi, double M,
-                                                 double dg, double d32, int64_t k) {
+                                                 double dg, double d32, double eg, int64_t k) {
     if (dg != dg || d32 != d32) {
         write_margin(margin, lo, hi, M, 0.0, k, 0x1p-53);
         margin[1] = __builtin_nan("");
@@ -166,7 +175,7 @@ __device__ __forceinline__ void write_margin_rec(double *margin, double lo, doub
         return;
     }
     const double u_gram = d32 > 0.0 ? 0x1p-24 : 0x1p-53;
-    write_margin(margin, lo, hi, M, dg, k, u_gram);
+    write_margin(margin, lo, hi, M, dg, k, u_gram, eg == eg ? eg : __builtin_inf());
     if (!(dg >= 1.0)) {
         margin[1] = __builtin_inf();
         margin[2] = 1.0;

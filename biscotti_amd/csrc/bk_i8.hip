@@ -1,0 +1,436 @@
+// bk_i8.hip -- K1i8: the Gram of fp32 rows from exact int8 slices (Ozaki
+// scheme), on v_mfma_i32_32x32x32_i8 (bk_set_f32_mode(ctx, BK_F32_I8);
+// BASELINE config E, 4096 x 262,144 fp32).
+//
+// The reference's Gram is np.dot(X, X.T) in fp64 (ML/code/logistic_validator.py:
+// 59-60).  Here the columns are cut into R ranges (one per XCD); within range r
+// row i is scaled by a power of two s_ir >= max_k |x_ik| and split into three
+// signed 7-bit digits,
+//     x_ik / s_ir = a0/64 + a1/2^13 + a2/2^20 + rho,   |a_t| <= 64, |rho| <= 2^-21,
+// all exact in fp64 (fp32 inputs, power-of-two scaling, integer subtractions).
+// The range's Gram is then
+//     P_r = s_i s_j 2^-26 (2^14 L0 + 2^7 L1 + L2),
+//     L0 = A0 A0^T,  L1 = A0 A1^T + A1 A0^T,  L2 = A0 A2^T + A1 A1^T + A2 A0^T,
+// six int8 GEMMs accumulated EXACTLY in int32 (|a a'| <= 2^12 per column,
+// <= 2^15 columns per range in practice, < 2^31), combined exactly in fp64
+// (< 2^53), so every range partial is exact for the truncated digits and the
+// whole Gram deterministic.  The dropped terms (a1 a2, a2 a1, a2 a2 and rho)
+// bound the error of every element absolutely (DESIGN.md §4 "K1i8"):
+//     |G_ij - G~_ij| <= sum_r 2^-21 (2 S_r L1_r + 2.03 d_r S_r^2) (1 + 2^-20),
+//     S_r = max_i s_ir,  L1_r = max_i ||x_i,r||_1,  d_r = the range's columns,
+// which k_i8_bound writes into the packed record's trailing element [2]; the
+// selection margin adds it to every distance (bk_device.h write_margin), so the
+// near-tie contract holds: a set that differs from the reference's comes with
+// near_tie = 1.  A non-finite input makes that bound +inf (always a near tie;
+// BK_F32_I8_CERTIFIED re-runs it exact).
+//
+//   k_i8_slice   one workgroup per (row, range): the range's max |x| and
+//                ||x||_1 (one read), then the three digit planes (a second read,
+//                from L2): HBM-bound, 4 + 3 bytes per element
+//   k_i8_bound   the absolute error bound (one workgroup)
+//   k_gram_i8    128 x 128 output tiles of one range per workgroup, 4 waves of
+//                64 x 64 (2 x 2 MFMA blocks x 3 levels: 192 int32 accumulators
+//                per lane), digit planes staged through LDS in chunks of 64
+//                columns (48 KiB per stage, 2 stages), 16-B granules
+//                XOR-swizzled so every ds_read_b128 fragment read is
+//                conflict-free; workgroup b runs range b mod R (= its XCD when
+//                R = 8) and the (b / R)-th tile of a super-blocked order, so the
+//                32 CUs of an XCD share their row-blocks through its L2
+//   k_i8_reduce  U = sum over ranges (fixed order) of the exact range partials,
+//                + the trailing record {d, 0, bound, 0}
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "bk_internal.h"
+
+namespace bk {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int I8_TILE = 128, I8_KC = 64, I8_S = 3;
+constexpr int I8_PLANE = I8_TILE * I8_KC;          // one digit plane of one operand per stage: 8 KiB
+constexpr int I8_OPND = I8_S * I8_PLANE;           // 24 KiB
+constexpr int I8_STAGE = 2 * I8_OPND;              // 48 KiB
+constexpr int I8_LDS = 2 * I8_STAGE;               // 96 KiB
+
+// ---------------------------------------------------------------------------
+// slicing: grid (npad rows, R ranges), 256 threads, 16 columns per thread-step
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_i8_slice(const float *__restrict__ X, int64_t ld, int n,
+                                                  int64_t d, const int64_t *__restrict__ rb, int R,
+                                                  int8_t *__restrict__ S, int64_t dp, int64_t plane,
+                                                  int *__restrict__ es, double *__restrict__ l1o) {
+    __shared__ float smx[4];
+    __shared__ double sl1[4];
+    __shared__ int sfin[4];
+    const int i = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+    const int64_t c0 = rb[r], c1 = rb[r + 1];
+    const int64_t ce = c1 < d ? c1 : d;  // columns past d are zero
+    const float *xr = X + (int64_t)i * ld;
+    float mx = 0.0f;
+    double l1 = 0.0;
+    int fin = 1;
+    if (i < n) {
+        for (int64_t c = c0 + (int64_t)tid * 4; c < ce; c += 1024) {
+            float v[4];
+            if (c + 4 <= ce) {
+                const float4 q = *reinterpret_cast<const float4 *>(xr + c);
+                v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = c + u < ce ? xr[c + u] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float a = __builtin_fabsf(v[u]);
+                fin &= a <= 3.4028235e38f;  // NaN and +-inf fail
+                mx = a > mx ? a : mx;
+                l1 += (double)a;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(mx, o);
+        mx = m2 > mx ? m2 : mx;
+        l1 += __shfl_xor(l1, o);
+        fin &= __shfl_xor(fin, o);
+    }
+    if ((tid & 63) == 0) {
+        smx[tid >> 6] = mx;
+        sl1[tid >> 6] = l1;
+        sfin[tid >> 6] = fin;
+    }
+    __syncthreads();
+    mx = smx[0];
+    l1 = sl1[0];
+    fin = sfin[0];
+    for (int w = 1; w < 4; ++w) {
+        mx = smx[w] > mx ? smx[w] : mx;
+        l1 += sl1[w];
+        fin &= sfin[w];
+    }
+    // s = 2^e > max |x| (frexp: mx = m 2^e, m in [0.5, 1)); all-zero rows: e = 0
+    int e = 0;
+    if (fin && mx > 0.0f) (void)frexpf(mx, &e);
+    if (tid == 0) {
+        es[(int64_t)i * R + r] = e;
+        l1o[(int64_t)i * R + r] = fin ? l1 : __builtin_inf();
+    }
+    int8_t *s0 = S + (int64_t)i * dp, *s1 = s0 + plane, *s2 = s1 + plane;
+    for (int64_t c = c0 + (int64_t)tid * 16; c < c1; c += 4096) {
+        int dig[3][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float v[4];
+            const int64_t cc = c + 4 * q;
+            if (i < n && fin && cc + 4 <= ce) {
+                const float4 f = *reinterpret_cast<const float4 *>(xr + cc);
+                v[0] = f.x, v[1] = f.y, v[2] = f.z, v[3] = f.w;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = (i < n && fin && cc + u < ce) ? xr[cc + u] : 0.0f;
+            }
+            int p0 = 0, p1 = 0, p2 = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double y = ldexp((double)v[u], 6 - e);  // 64 x / s, exact
+                const double a0 = __builtin_rint(y);
+                const double y1 = (y - a0) * 128.0;  // exact
+                const double a1 = __builtin_rint(y1);
+                const double a2 = __builtin_rint((y1 - a1) * 128.0);
+                p0 |= ((int)a0 & 0xff) << (8 * u);
+                p1 |= ((int)a1 & 0xff) << (8 * u);
+                p2 |= ((int)a2 & 0xff) << (8 * u);
+            }
+            dig[0][q] = p0;
+            dig[1][q] = p1;
+            dig[2][q] = p2;
+        }
+        *reinterpret_cast<v4i *>(s0 + c) = v4i{dig[0][0], dig[0][1], dig[0][2], dig[0][3]};
+        *reinterpret_cast<v4i *>(s1 + c) = v4i{dig[1][0], dig[1][1], dig[1][2], dig[1][3]};
+        *reinterpret_cast<v4i *>(s2 + c) = v4i{dig[2][0], dig[2][1], dig[2][2], dig[2][3]};
+    }
+}
+
+// the absolute error bound of the sliced Gram (header), into out[0]
+__global__ __launch_bounds__(256) void k_i8_bound(const int *__restrict__ es,
+                                                  const double *__restrict__ l1,
+                                                  const int64_t *__restrict__ rb, int R, int n,
+                                                  int64_t d, double *__restrict__ out) {
+    __shared__ double ssm[4], slm[4];
+    double tot = 0.0;
+    for (int r = 0; r < R; ++r) {
+        double smax = 0.0, lmax = 0.0;
+        for (int i = threadIdx.x; i < n; i += 256) {
+            const double s = ldexp(1.0, es[(int64_t)i * R + r]);
+            const double v = l1[(int64_t)i * R + r];
+            smax = s > smax ? s : smax;
+            lmax = (v > lmax || v != v) ? v : lmax;  // a NaN / inf norm poisons the bound
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double a = __shfl_xor(smax, o), b = __shfl_xor(lmax, o);
+            smax = a > smax ? a : smax;
+            lmax = (b > lmax || b != b) ? b : lmax;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            ssm[threadIdx.x >> 6] = smax;
+            slm[threadIdx.x >> 6] = lmax;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < 4; ++w) {
+                smax = ssm[w] > smax ? ssm[w] : smax;
+                lmax = (slm[w] > lmax || slm[w] != slm[w]) ? slm[w] : lmax;
+            }
+            smax = ssm[0] > smax ? ssm[0] : smax;
+            lmax = (slm[0] > lmax || slm[0] != slm[0]) ? slm[0] : lmax;
+            const int64_t c1 = rb[r + 1] < d ? rb[r + 1] : d;
+            const double dr = (double)(c1 > rb[r] ? c1 - rb[r] : 0);
+            tot += 0x1p-21 * (2.0 * smax * lmax + 2.03 * dr * smax * smax);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = (tot == tot && tot < __builtin_inf()) ? tot * (1.0 + 0x1p-20)
+                                                                         : __builtin_inf();
+}
+
+// ---------------------------------------------------------------------------
+// the int8 Gram: one 128 x 128 tile of one range per workgroup
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int i8_swz(int row, int g) { return g ^ ((row >> 2) & 3); }
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
+               const int64_t *__restrict__ rb, int R, const int2 *__restrict__ order,
+               const int *__restrict__ es, int n, int T64, double *__restrict__ part,
+               int64_t ntile64) {
+    extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = blockIdx.x % R;
+    const int2 tile = order[blockIdx.x / R];
+    const int I = tile.x, J = tile.y;
+    const int64_t k0 = rb[r], k1 = rb[r + 1];
+    const int nch = (int)((k1 - k0) / I8_KC);
+    // staging: granule (operand o, digit t, row, g) of the chunk; thread t
+    // moves 12: index q = tid + 256 u -> g = q & 3, row = (q >> 2) & 127,
+    // t = (q >> 9) % 3, o = q / 1536
+    const int8_t *src[12];
+    int dst[12];
+#pragma unroll
+    for (int u = 0; u < 12; ++u) {
+        const int q = tid + 256 * u;
+        const int g = q & 3, row = (q >> 2) & 127, t = (q >> 9) % 3, o = q / 1536;
+        const int grow = (o == 0 ? I : J) * I8_TILE + row;
+        src[u] = S + (int64_t)t * plane + (int64_t)grow * dp + k0 + 16 * g;
+        dst[u] = o * I8_OPND + t * I8_PLANE + row * I8_KC + 16 * i8_swz(row, g);
+    }
+    v4i pf[12];
+    auto fetch = [&](int ch) {
+#pragma unroll
+        for (int u = 0; u < 12; ++u) pf[u] = *reinterpret_cast<const v4i *>(src[u] + (int64_t)ch * I8_KC);
+    };
+    auto put = [&](int stage) {
+        int8_t *b = lds + stage * I8_STAGE;
+#pragma unroll
+        for (int u = 0; u < 12; ++u) *reinterpret_cast<v4i *>(b + dst[u]) = pf[u];
+    };
+    v16i acc[3][2][2];
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[l][a][b] = v16i{};
+    const int wr = (wave & 1) * 64, wc = (wave >> 1) * 64;
+    const int fr = lane & 31, fh = lane >> 5;
+    if (nch > 0) {
+        fetch(0);
+        put(0);
+        if (nch > 1) fetch(1);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int8_t *b = lds + (ch & 1) * I8_STAGE;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int g = 2 * ks + fh;
+            v4i fa[3][2], fb[3][2];
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    const int ra = wr + 32 * a + fr, rbw = wc + 32 * a + fr;
+                    fa[t][a] = *reinterpret_cast<const v4i *>(b + t * I8_PLANE + ra * I8_KC +
+                                                              16 * i8_swz(ra, g));
+                    fb[t][a] = *reinterpret_cast<const v4i *>(b + I8_OPND + t * I8_PLANE +
+                                                              rbw * I8_KC + 16 * i8_swz(rbw, g));
+                }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb) {
+                    acc[0][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[0][bb], acc[0][a][bb], 0, 0, 0);
+                    acc[1][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[1][bb], acc[1][a][bb], 0, 0, 0);
+                    acc[1][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][a], fb[0][bb], acc[1][a][bb], 0, 0, 0);
+                    acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[2][bb], acc[2][a][bb], 0, 0, 0);
+                    acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][a], fb[1][bb], acc[2][a][bb], 0, 0, 0);
+                    acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][a], fb[0][bb], acc[2][a][bb], 0, 0, 0);
+                }
+        }
+        // the next chunk into the other stage (its previous readers finished
+        // at the barrier that ended chunk ch - 1), then prefetch ch + 2
+        if (ch + 1 < nch) {
+            put((ch + 1) & 1);
+            if (ch + 2 < nch) fetch(ch + 2);
+        }
+        __syncthreads();
+    }
+    // epilogue: C/D lane l, reg e of a 32 x 32 block: row (e & 3) + 8 (e >> 2) + 4 (l >> 5), col l & 31
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int gj = J * I8_TILE + wc + 32 * bb + fr;
+            const int bj = gj >> 6;
+            const int ej = gj < n ? es[(int64_t)gj * R + r] : 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int gi = I * I8_TILE + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * fh;
+                const int bi = gi >> 6;
+                if (bi > bj || bj >= T64) continue;  // the lower half of a diagonal tile; padding
+                const int ei = gi < n ? es[(int64_t)gi * R + r] : 0;
+                const double v = (double)acc[0][a][bb][e] * 16384.0 + (double)acc[1][a][bb][e] * 128.0 +
+                                 (double)acc[2][a][bb][e];
+                const int64_t u = (int64_t)bi * T64 - (int64_t)bi * (bi - 1) / 2 + (bj - bi);
+                part[((int64_t)r * ntile64 + u) * 4096 + (gi & 63) * 64 + (gj & 63)] =
+                    ldexp(v, ei + ej - 26);
+            }
+        }
+}
+
+// U = sum over the R ranges, in order; the trailing record {d, 0, bound, 0}
+__global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ part, int R,
+                                                   int64_t usz, double *__restrict__ U, double d,
+                                                   const double *__restrict__ bound) {
+    const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (e < usz) {
+        d2v acc = *reinterpret_cast<const d2v *>(part + e);
+        for (int r = 1; r < R; ++r) {
+            const d2v v = *reinterpret_cast<const d2v *>(part + (int64_t)r * usz + e);
+            acc.x += v.x;
+            acc.y += v.y;
+        }
+        *reinterpret_cast<d2v *>(U + e) = acc;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        U[usz] = d;
+        U[usz + 1] = 0.0;
+        U[usz + 2] = bound[0];
+        U[usz + 3] = 0.0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+I8Layout i8_layout(int n, int64_t d) {
+    I8Layout L;
+    L.npad = (n + I8_TILE - 1) / I8_TILE * I8_TILE;
+    L.dp = (d + I8_KC - 1) / I8_KC * I8_KC;
+    const int64_t nk = L.dp / I8_KC;
+    L.R = (int)(nk < 8 ? nk : 8);
+    L.rb.resize(L.R + 1);
+    for (int r = 0; r <= L.R; ++r) L.rb[r] = nk * r / L.R * I8_KC;
+    L.plane = (int64_t)L.npad * L.dp;
+    L.T128 = L.npad / I8_TILE;
+    L.T64 = (n + 63) / 64;
+    L.ntile64 = (int64_t)L.T64 * (L.T64 + 1) / 2;
+    // super-blocked upper-triangle order of the 128-row tiles: blocks of 4 x 4
+    // tiles row by row, so the CUs of an XCD, which take consecutive tiles,
+    // share their row-blocks through its L2
+    constexpr int SB = 4;
+    const int T = L.T128, NB = (T + SB - 1) / SB;
+    for (int BI = 0; BI < NB; ++BI)
+        for (int BJ = BI; BJ < NB; ++BJ)
+            for (int I = BI * SB; I < BI * SB + SB && I < T; ++I)
+                for (int J = BJ * SB; J < BJ * SB + SB && J < T; ++J)
+                    if (I <= J) {
+                        L.order.push_back(I);
+                        L.order.push_back(J);
+                    }
+    return L;
+}
+
+size_t i8_workspace(const I8Layout &L) {
+    // digit planes, rb, order, exponents, norms, bound, range partials
+    return (size_t)I8_S * L.plane + 256 + (size_t)(L.R + 1) * 8 + L.order.size() * 4 + 256 +
+           (size_t)L.npad * L.R * (4 + 8) + 256 + 256 +
+           (size_t)L.R * L.ntile64 * 4096 * 8 + 256;
+}
+
+hipError_t configure_i8_kernels() {
+    return hipFuncSetAttribute((const void *)k_gram_i8, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               I8_LDS);
+}
+
+static char *align256(char *p) { return (char *)(((uintptr_t)p + 255) & ~(uintptr_t)255); }
+
+// the workspace's pieces (i8_workspace)
+struct I8Ws {
+    int8_t *S;
+    int *es;
+    double *l1, *bound, *part;
+};
+static I8Ws i8_ws(const I8Layout &L, void *ws) {
+    I8Ws w;
+    char *p = align256((char *)ws);
+    w.S = (int8_t *)p;
+    p = align256(p + (size_t)I8_S * L.plane);
+    w.es = (int *)p;
+    p = align256(p + (size_t)L.npad * L.R * 4);
+    w.l1 = (double *)p;
+    p = align256(p + (size_t)L.npad * L.R * 8);
+    w.bound = (double *)p;
+    p = align256(p + 256);
+    w.part = (double *)p;
+    return w;
+}
+
+hipError_t launch_i8_slice(const float *X, int64_t ld, int n, int64_t d, const I8Layout &L,
+                           void *ws, const void *tables, hipStream_t st) {
+    const I8Ws w = i8_ws(L, ws);
+    const int64_t *rb = (const int64_t *)tables;
+    hipLaunchKernelGGL(k_i8_slice, dim3((unsigned)L.npad, (unsigned)L.R), dim3(256), 0, st, X, ld, n,
+                       d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_i8_bound, dim3(1), dim3(256), 0, st, w.es, w.l1, rb, L.R, n, d, w.bound);
+    return hipGetLastError();
+}
+
+hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables, hipStream_t st) {
+    const I8Ws w = i8_ws(L, ws);
+    const int64_t *rb = (const int64_t *)tables;  // {rb (R + 1 int64), order (int pairs)}
+    const int2 *order = (const int2 *)((const char *)tables + (size_t)(L.R + 1) * 8);
+    const int64_t ntiles = (int64_t)L.order.size() / 2;
+    hipLaunchKernelGGL(k_gram_i8, dim3((unsigned)(ntiles * L.R)), dim3(256), I8_LDS, st, w.S, L.dp,
+                       L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
+    return hipGetLastError();
+}
+
+hipError_t launch_i8_reduce(int64_t d, const I8Layout &L, void *ws, double *U, hipStream_t st) {
+    const I8Ws w = i8_ws(L, ws);
+    const int64_t usz = L.ntile64 * 4096;
+    hipLaunchKernelGGL(k_i8_reduce, dim3((unsigned)((usz / 2 + 255) / 256)), dim3(256), 0, st, w.part,
+                       L.R, usz, U, (double)d, w.bound);
+    return hipGetLastError();
+}
+
+}  // namespace bk

@@ -11,6 +11,11 @@
 
 namespace bk {
 
+// the packed upper's trailing record (bk_upper_elems): {column count, columns
+// accumulated on the fp32 MFMA, absolute Gram error bound of the int8-sliced
+// columns (K1i8), 0}; every exchange sums it with the tiles
+constexpr int BK_UPPER_TRAIL = 4;
+
 // Probe knobs: timing-only ablations (BK_GRAM_MODE, BK_K2_MODE), planner and
 // kernel-shape overrides and debug traces, read only by A/B builds
 // (build(extra=["-DBK_PROBES"], out=tools/ab/...)).  The product libbk.so
@@ -169,6 +174,26 @@ hipError_t launch_roni_softmax_batches(const float *Xv, int64_t nv, int64_t din,
                                        const double *deltas, int64_t n, int64_t ld,
                                        const int64_t *idx, int64_t nb, double *scores,
                                        int32_t *near_out, hipStream_t st);
+// bk_i8.hip: K1i8, the Gram of fp32 rows from exact int8 digit slices
+// (BK_F32_I8): column ranges (one per XCD), digit planes [3][npad][dp] int8
+struct I8Layout {
+    int npad = 0, R = 0, T128 = 0, T64 = 0;
+    int64_t dp = 0, plane = 0, ntile64 = 0;
+    std::vector<int64_t> rb;  // range boundaries (R + 1, multiples of 64 columns)
+    std::vector<int> order;   // the 128-row tiles (I <= J), super-blocked: pairs
+};
+I8Layout i8_layout(int n, int64_t d);
+size_t i8_workspace(const I8Layout &L);
+hipError_t configure_i8_kernels();
+// tables: device copy of {rb (R + 1 int64), order (int pairs)}; ws:
+// i8_workspace(L) bytes.  slice: digit planes + the error bound; gemm: the
+// range partials; reduce: U (bk_upper_elems(n)) with the trailing record
+// {d, 0, bound, 0}
+hipError_t launch_i8_slice(const float *X, int64_t ld, int n, int64_t d, const I8Layout &L,
+                           void *ws, const void *tables, hipStream_t st);
+hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables, hipStream_t st);
+hipError_t launch_i8_reduce(int64_t d, const I8Layout &L, void *ws, double *U, hipStream_t st);
+
 // bk_small.hip: the whole Multi-Krum of a small batch (n <= 128) in one launch
 struct SmallPlan {
     int nb16 = 0, nblk = 0, kc = 0, P = 0, ng = 0, Q = 0, nS = 0, C = 0;  // P chunks, ng G items

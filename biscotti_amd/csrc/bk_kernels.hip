@@ -874,6 +874,8 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         U[usz] = dcols;
         U[usz + 1] = dcols32;
+        U[usz + 2] = 0.0;  // no int8-sliced columns
+        U[usz + 3] = 0.0;
     }
 #ifndef BK_REDUCE_V1
     // 64 elements per block, 2 per lane (16-B loads), 8 slabs in flight per
@@ -951,6 +953,8 @@ __global__ __launch_bounds__(256) void k_reduce(const double *__restrict__ part,
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // as k_reduce3 (v1 never runs the fp32 MFMA)
         U[(int64_t)ntile * 4096] = dcols;
         U[(int64_t)ntile * 4096 + 1] = 0.0;
+        U[(int64_t)ntile * 4096 + 2] = 0.0;
+        U[(int64_t)ntile * 4096 + 3] = 0.0;
     }
     const int u = blockIdx.x >> 4, chunk = blockIdx.x & 15;
     const int e = chunk * 256 + threadIdx.x;
@@ -1475,9 +1479,10 @@ __global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, 
     if (tid == 0) {
         double M = 0.0;
         for (int w = 0; w < 16; ++w) M = fmax(M, mx[w]);
-        // the packed record's trailing pair: the Gram's column count and the
-        // part of it accumulated on the fp32 MFMA (after an exchange: totals)
-        write_margin_rec(margin, bnd[0], bnd[1], M, dcols[0], dcols[1], k);
+        // the packed record's trailing record: the Gram's column count, the
+        // part of it accumulated on the fp32 MFMA and the int8-sliced columns'
+        // absolute error bound (after an exchange: totals)
+        write_margin_rec(margin, bnd[0], bnd[1], M, dcols[0], dcols[1], dcols[2], k);
     }
 }
 

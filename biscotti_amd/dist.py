@@ -34,11 +34,12 @@ def all_shards(d, world, align=ALIGN):
 
 
 def upper_elems(n):
-    """bk_upper_elems: the 64x64 upper sub-tiles + the trailing pair {column
-    count, columns accumulated on the fp32 MFMA} (summed by the exchange with
-    the tiles; the selection margin's d and unit roundoff)."""
+    """bk_upper_elems: the 64x64 upper sub-tiles + the trailing record {column
+    count, columns accumulated on the fp32 MFMA, the int8-sliced Gram's absolute
+    error bound, 0} (summed by the exchange with the tiles; the selection
+    margin's d, unit roundoff and Gram error)."""
     T = (n + 63) // 64
-    return T * (T + 1) // 2 * 4096 + 2
+    return T * (T + 1) // 2 * 4096 + 4
 
 
 def pack_upper(G, d_cols, d_cols_f32=0):
@@ -60,7 +61,7 @@ def pack_upper(G, d_cols, d_cols_f32=0):
         for bj in range(bi, T):
             out[u] = Gp[bi * 64:(bi + 1) * 64, bj * 64:(bj + 1) * 64]
             u += 1
-    return np.concatenate([out.reshape(-1), [float(d_cols), float(d_cols_f32)]])
+    return np.concatenate([out.reshape(-1), [float(d_cols), float(d_cols_f32), 0.0, 0.0]])
 
 
 def unpack_upper(U, n):

@@ -134,7 +134,28 @@ int bk_graph_enable(bk_ctx *ctx, int on);
  * config E: the selection matches wherever the score gap at the boundary
  * exceeds the fp32 Gram error bound (~2 k gamma_d max|x_i|^2).  The mean is
  * unchanged (fp64 accumulation of the fp32 rows).  No effect on fp64 rows. */
-enum bk_f32_mode { BK_F32_EXACT = 0, BK_F32_MFMA = 1, BK_F32_CERTIFIED = 2 };
+enum bk_f32_mode {
+    BK_F32_EXACT = 0,
+    BK_F32_MFMA = 1,
+    BK_F32_CERTIFIED = 2,
+    BK_F32_I8 = 3,
+    BK_F32_I8_CERTIFIED = 4
+};
+/* BK_F32_I8: the Gram from exact int8 digit slices on v_mfma_i32_32x32x32_i8
+ * (bk_i8.hip, K1i8; the Ozaki scheme).  Per range of columns (one per XCD)
+ * every row is scaled by a power of two >= its max |x| and cut into three
+ * signed 7-bit digits; the six digit products of weight >= 2^-26 accumulate
+ * exactly in int32 and combine exactly in fp64, so each range's partial is
+ * exact for the truncated digits and the result deterministic.  The dropped
+ * digits bound every Gram element's error ABSOLUTELY by
+ *     sum_r 2^-21 (2 S_r L1_r + 2.03 d_r S_r^2)
+ * (S_r the largest row scale, L1_r the largest ||x_i||_1 of range r, d_r its
+ * columns), carried in the packed record and added to the selection margin's
+ * bound: a selection that differs from the reference's comes with near_tie = 1.
+ * Far tighter than the fp32 MFMA's gamma_d (config E: ~1e-4 against ~1.6e-2 of
+ * max |x_i|^2) and several times faster.  Rows must be 16-B aligned (ld % 4 ==
+ * 0, aligned base) and d >= 64; other batches take the exact path.  A
+ * non-finite input makes the bound +inf (a near tie). */
 /* BK_F32_CERTIFIED: the fp32 MFMA, then -- only when the selection margin
  * (bk_selection_margin) does not clear the fp32 bound -- the exact path on the
  * same device-resident batch, whose outputs replace the first run's.  Never
@@ -145,7 +166,8 @@ enum bk_f32_mode { BK_F32_EXACT = 0, BK_F32_MFMA = 1, BK_F32_CERTIFIED = 2 };
  * group's contexts (bk_group_ctx): a near tie re-runs every device's shard
  * exact from device memory, then exchanges and finishes again. */
 int bk_set_f32_mode(bk_ctx *ctx, int mode);
-/* exact re-runs BK_F32_CERTIFIED has made on this context */
+/* BK_F32_I8_CERTIFIED: the same contract on the int8-sliced Gram.
+ * exact re-runs BK_F32_CERTIFIED / BK_F32_I8_CERTIFIED have made on this context */
 int64_t bk_certified_reruns(bk_ctx *ctx);
 
 /* ---- selection margin: where the selection may legitimately differ from the
@@ -415,7 +437,8 @@ enum bk_kernel_id {
     BK_K_NOISE = 13,     /* K6  noise application (bk_noise_apply_device)      */
     BK_K_RONI = 14,      /* K7  RONI counts + scores (bk_roni*)                 */
     BK_K_SMALL = 15,     /* K1..K4 fused in one launch for n <= 128 (k_small)   */
-    BK_NUM_KERNELS = 16
+    BK_K_SLICE = 16,     /* K1i8 digit slicing + error bound (BK_F32_I8)        */
+    BK_NUM_KERNELS = 17
 };
 int bk_timing_enable(bk_ctx *ctx, int on);   /* all kernels; clears accumulated timings */
 /* Time only the kernels whose bit (1u << kernel_id) is set: every timed kernel

@@ -44,7 +44,7 @@ def test_abi_version_and_names():
     assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 10
     assert L.bk_kernel_name(0) == b"k_gram"
     assert L.bk_kernel_name(99) == b"?"
-    assert len(_lib.KERNELS) == 16
+    assert len(_lib.KERNELS) == 17
     for i, name in enumerate(_lib.KERNELS):
         assert L.bk_kernel_name(i) == name.encode()
 
@@ -59,13 +59,14 @@ def test_check_args(n, d, f, status):
 
 
 def test_upper_elems():
-    """64x64 upper sub-tiles + the trailing pair {column count, fp32-MFMA columns}."""
+    """64x64 upper sub-tiles + the trailing record {column count, fp32-MFMA
+    columns, int8 Gram error bound, 0}."""
     from biscotti_amd import dist as D
     L = _lib.lib()
-    assert L.bk_upper_elems(1) == 4096 + 2
-    assert L.bk_upper_elems(64) == 4096 + 2
-    assert L.bk_upper_elems(65) == 3 * 4096 + 2
-    assert L.bk_upper_elems(512) == 36 * 4096 + 2
+    assert L.bk_upper_elems(1) == 4096 + 4
+    assert L.bk_upper_elems(64) == 4096 + 4
+    assert L.bk_upper_elems(65) == 3 * 4096 + 4
+    assert L.bk_upper_elems(512) == 36 * 4096 + 4
     for n in (1, 63, 64, 65, 512, 4097):
         assert D.upper_elems(n) == L.bk_upper_elems(n)
 

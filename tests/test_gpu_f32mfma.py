@@ -49,11 +49,12 @@ def test_layout_exact_on_small_integers(engine, n, d):
         got = _upper(engine, X)
     finally:
         engine.set_f32_mode(_lib.BK_F32_EXACT)
-    assert np.array_equal(got[:-2], want[:-2])  # the tiles, bit for bit
-    # the trailing pair: the column count, and the columns taken on the fp32
+    assert np.array_equal(got[:-4], want[:-4])  # the tiles, bit for bit
+    # the trailing record: the column count, and the columns taken on the fp32
     # MFMA (the K1 v3 kernel, 16-B aligned rows; v1 has no fp32 MFMA)
-    assert got[-2] == want[-2] == d and want[-1] == 0.0
-    assert got[-1] == (d if d % 4 == 0 else 0.0)
+    assert got[-4] == want[-4] == d and want[-3] == 0.0
+    assert got[-3] == (d if d % 4 == 0 else 0.0)
+    assert got[-2] == want[-2] == 0.0 and got[-1] == want[-1] == 0.0
 
 
 def test_clustered_vs_oracle(f32eng, oracle):

@@ -1,0 +1,225 @@
+"""MI355X: K1i8, the Gram of fp32 rows from exact int8 digit slices
+(bk_set_f32_mode(ctx, BK_F32_I8); bk_i8.hip; BASELINE config E, VERDICT r3
+item 4).  The reference's Gram is np.dot(X, X.T) in fp64
+(ML/code/logistic_validator.py:59-60).
+
+* Layout and exactness: rows whose values are small integers times a per-row
+  power of two are represented exactly by the digits, so the int8 Gram must
+  equal the exact fp64 one BIT FOR BIT (ragged n and d, one to eight column
+  ranges, the diagonal 128-row tiles and the padding).
+* The absolute error bound: on random rows every element of the int8 Gram lies
+  within the record's bound (its trailing element [2], recomputed here from
+  the definition) of the exact Gram.
+* Multi-Krum: every fp32 golden (config E at full size, its tight variant, the
+  700 x 65,536 tight case): the selection equals the reference's, or the call is
+  flagged near_tie with gap <= err_bound; BK_F32_I8_CERTIFIED always returns
+  the reference's set.  The margin record matches its definition with the int8
+  term.
+* Non-finite input: the bound is +inf (always a near tie).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from biscotti_amd import _lib  # noqa: E402
+import golden_util as GU  # noqa: E402
+
+
+def _upper(engine, X, mode):
+    n, d = X.shape
+    tX = torch.from_numpy(np.ascontiguousarray(X)).cuda()
+    U = torch.empty(int(_lib.lib().bk_upper_elems(n)), dtype=torch.float64, device="cuda")
+    engine.set_f32_mode(mode)
+    try:
+        engine.gram_upper_ptr(tX.data_ptr(), _lib.BK_F32, n, d, d, U.data_ptr())
+        engine.synchronize()
+    finally:
+        engine.set_f32_mode(_lib.BK_F32_EXACT)
+    return U.cpu().numpy()
+
+
+def _ranges(d):
+    dp = (d + 63) // 64 * 64
+    nk = dp // 64
+    R = min(nk, 8)
+    return [(nk * r // R * 64, nk * (r + 1) // R * 64) for r in range(R)]
+
+
+def _bound(X):
+    """bk_i8.hip's absolute bound, restated from its definition."""
+    X = X.astype(np.float64)
+    tot = 0.0
+    for c0, c1 in _ranges(X.shape[1]):
+        A = np.abs(X[:, c0:min(c1, X.shape[1])])
+        if A.shape[1] == 0:
+            continue
+        mx = A.max(1)
+        s = np.where(mx > 0, 2.0 ** np.where(mx > 0, np.frexp(mx)[1], 0), 1.0)
+        S, L1 = float(s.max()), float(A.sum(1).max())
+        tot += 2.0 ** -21 * (2.0 * S * L1 + 2.03 * A.shape[1] * S * S)
+    return tot * (1.0 + 2.0 ** -20)
+
+
+@pytest.mark.parametrize("n,d", [(129, 64), (130, 4096), (256, 4160), (300, 20000), (512, 4000),
+                                 (1000, 777), (200, 70000)])
+def test_exact_on_scaled_small_integers(engine, n, d):
+    rng = np.random.default_rng(n + d)
+    X = rng.integers(-64, 65, size=(n, d)).astype(np.float32)
+    X *= (2.0 ** rng.integers(-10, 11, size=(n, 1))).astype(np.float32)  # per-row scales
+    X[3] = 0.0  # an all-zero row
+    want = _upper(engine, X, _lib.BK_F32_EXACT)
+    got = _upper(engine, X, _lib.BK_F32_I8)
+    assert np.array_equal(got[:-4], want[:-4])  # the tiles, bit for bit
+    assert got[-4] == d and got[-3] == 0.0 and got[-1] == 0.0
+    assert got[-2] == pytest.approx(_bound(X), rel=1e-12)
+
+
+@pytest.mark.parametrize("n,d,scale", [(257, 3000, 1.0), (640, 65536, 1e-3), (1024, 20000, 1e4),
+                                       (150, 100000, 1.0)])
+def test_error_within_the_bound(engine, n, d, scale):
+    from biscotti_amd.dist import unpack_upper
+    rng = np.random.default_rng(d)
+    X = (scale * rng.standard_normal((n, d))).astype(np.float32)
+    X[: n // 4] *= np.float32(1e-3)  # rows of very different magnitude
+    want = unpack_upper(_upper(engine, X, _lib.BK_F32_EXACT), n)
+    U = _upper(engine, X, _lib.BK_F32_I8)
+    got = unpack_upper(U, n)
+    E = float(U[-2])
+    assert E == pytest.approx(_bound(X), rel=1e-12)
+    err = float(np.max(np.abs(got - want)))
+    print("K1i8 n=%d d=%d: max |G~ - G| %.3e, bound %.3e, max G_ii %.3e"
+          % (n, d, err, E, float(np.max(np.diag(want)))))
+    assert err <= E
+    assert np.array_equal(got, got.T)  # symmetric bit for bit
+
+
+def _device_batch(engine, name):
+    p = GU.C.case_params(name)
+    n, d = p["n"], p["d"]
+    X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F32, n, d, d, 0, d, p["seed"], p["nbyz"],
+                          p["mu_scale"], p["byz_scale"], p["sigma"], p["flags"])
+    return X, p
+
+
+def _run(engine, X, f):
+    n, d = X.shape
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    sc = torch.empty(n, dtype=torch.float64, device="cuda")
+    mean = torch.empty(d, dtype=torch.float64, device="cuda")
+    engine.multikrum_device_ptr(X.data_ptr(), _lib.BK_F32, n, d, d, f, sel.data_ptr(),
+                                sc.data_ptr(), mean.data_ptr())
+    engine.synchronize()
+    return sel.cpu().numpy(), sc.cpu().numpy(), mean.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", [k for k in ("E_4096x262144_fp32", "E_tight_fp32",
+                                               "fp32_tight_700x65536", "fp32_200x3000")
+                                  if GU.have(k)])
+def test_i8_matches_or_flags(name, engine):
+    X, p = _device_batch(engine, name)
+    n, d, f = p["n"], p["d"], p["f"]
+    g = GU.load(name)
+    try:
+        engine.set_f32_mode(_lib.BK_F32_I8)
+        sel, sc, mean = _run(engine, X, f)
+        mg = engine.selection_margin()
+        assert mg["near_tie"] == (not (mg["gap"] > mg["err_bound"]))
+        if not np.array_equal(sel, g["sel"]):
+            assert mg["near_tie"] and not mg["gap"] > mg["err_bound"], mg
+        else:
+            GU.check_mean(mean, g, GU.manifest()[name])
+        if name == "E_4096x262144_fp32":  # the config-E golden's gap clears the int8 bound
+            assert not mg["near_tie"] and np.array_equal(sel, g["sel"])
+        k = n - f - 2
+        err = float(np.max(np.abs(sc - g["scores"])))
+        print("%s K1i8: max score error %.3e, err_bound %.3e, gap %.3e, near_tie %s"
+              % (name, err, mg["err_bound"], mg["gap"], mg["near_tie"]))
+        assert err <= mg["err_bound"] / 2 + 1e-9 * float(np.max(np.abs(g["scores"])))
+        flagged = mg["near_tie"]
+        engine.set_f32_mode(_lib.BK_F32_I8_CERTIFIED)
+        r0 = engine.certified_reruns()
+        sel2, sc2, mean2 = _run(engine, X, f)
+        assert np.array_equal(sel2, g["sel"])
+        assert engine.certified_reruns() - r0 == (1 if flagged else 0)
+        GU.check_mean(mean2, g, GU.manifest()[name])
+        assert k == mg["k"]
+    finally:
+        engine.set_f32_mode(_lib.BK_F32_EXACT)
+    del X
+    torch.cuda.empty_cache()
+
+
+def test_i8_margin_record(engine, oracle):
+    """The device margin record of an int8 call against its definition: the
+    gap from the call's own scores, the bound with the record's int8 term."""
+    n, d, f = 300, 20000, 90
+    rng = np.random.default_rng(3)
+    mu = 0.01 * rng.standard_normal(d)
+    X = (mu + 1e-3 * rng.standard_normal((n, d))).astype(np.float32)
+    byz = rng.choice(n, f, replace=False)
+    X[byz] += (0.05 * rng.standard_normal((f, d))).astype(np.float32)
+    engine.set_f32_mode(_lib.BK_F32_I8)
+    try:
+        sel, sc, mean = engine.multikrum(X, f)
+        mg = engine.selection_margin()
+    finally:
+        engine.set_f32_mode(_lib.BK_F32_EXACT)
+    osel, osc, omean = oracle.krum(X, f)
+    assert np.array_equal(sel, osel) and not mg["near_tie"]
+    GU.check_margin(mg, sc, oracle.sqnorms(X), n, f, d, eg=_bound(X))
+    X64 = X.astype(np.float64)
+    scale = np.max(np.abs(X64[osel]).sum(0) / len(osel))
+    assert np.max(np.abs(mean - omean)) <= 1e-9 * scale
+
+
+def test_i8_nonfinite_is_a_near_tie(engine):
+    n, d, f = 200, 5000, 60
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X[17, 123] = np.inf
+    U = _upper(engine, X, _lib.BK_F32_I8)
+    assert U[-2] == np.inf
+    engine.set_f32_mode(_lib.BK_F32_I8)
+    try:
+        engine.multikrum(X, f)
+        assert engine.selection_margin()["near_tie"]
+    finally:
+        engine.set_f32_mode(_lib.BK_F32_EXACT)
+
+
+def test_i8_shard_records_sum(engine):
+    """Two column shards on the int8 path: each record carries its own bound,
+    and the exchange's sum (here: on the host) finishes like the whole batch."""
+    from biscotti_amd.dist import all_shards
+    n, d, f = 400, 30000, 120
+    rng = np.random.default_rng(5)
+    X = (0.01 * rng.standard_normal((n, d))).astype(np.float32)
+    tX = torch.from_numpy(X).cuda()
+    usz = int(_lib.lib().bk_upper_elems(n))
+    acc = torch.zeros(usz, dtype=torch.float64, device="cuda")
+    bounds = []
+    engine.set_f32_mode(_lib.BK_F32_I8)
+    try:
+        for c0, dl in all_shards(d, 2):
+            U = torch.empty(usz, dtype=torch.float64, device="cuda")
+            Xs = np.ascontiguousarray(X[:, c0:c0 + dl])
+            tXs = torch.from_numpy(Xs).cuda()
+            engine.gram_upper_ptr(tXs.data_ptr(), _lib.BK_F32, n, dl, dl, U.data_ptr())
+            engine.synchronize()
+            assert float(U[-4]) == dl and float(U[-2]) == pytest.approx(_bound(Xs), rel=1e-12)
+            bounds.append(float(U[-2]))
+            acc += U
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        sc = torch.empty(n, dtype=torch.float64, device="cuda")
+        engine.finish_ptr(acc.data_ptr(), tX.data_ptr(), _lib.BK_F32, n, d, d, f, sel.data_ptr(),
+                          sc.data_ptr(), None)
+        engine.synchronize()
+        mg = engine.selection_margin()
+    finally:
+        engine.set_f32_mode(_lib.BK_F32_EXACT)
+    assert mg["d"] == d
+    want = GU.margin_bound(mg["M"], d, n - f - 2, eg=sum(bounds))
+    assert abs(mg["err_bound"] - want) <= 1e-12 * want

@@ -148,7 +148,7 @@ def test_certified_host_entry(engine, oracle):
 
 
 def test_margin_of_summed_shards_counts_all_columns(engine):
-    """The packed partials' trailing pairs sum to the total d (and to 0 fp32-MFMA
+    """The packed partials' trailing records sum to the total d (and to 0 fp32-MFMA
     columns), so the margin after a multi-GPU exchange uses the whole batch's
     column count."""
     from biscotti_amd.dist import all_shards
@@ -161,7 +161,7 @@ def test_margin_of_summed_shards_counts_all_columns(engine):
         U = torch.empty(usz, dtype=torch.float64, device="cuda")
         engine.gram_upper_ptr(X[:, c0:].data_ptr(), _lib.BK_F64, n, dl, X.stride(0), U.data_ptr())
         engine.synchronize()
-        assert float(U[-2]) == dl and float(U[-1]) == 0.0
+        assert float(U[-4]) == dl and float(U[-3]) == 0.0 and float(U[-2]) == 0.0
         acc += U
     sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
     sc = torch.empty(n, dtype=torch.float64, device="cuda")
@@ -214,8 +214,8 @@ def test_f32_mfma_record_carries_its_roundoff(engine, oracle):
             U = torch.empty(usz, dtype=torch.float64, device="cuda")
             eng.gram_upper_ptr(X[:, c0:].data_ptr(), _lib.BK_F32, n, dl, X.stride(0), U.data_ptr())
             eng.synchronize()
-            assert float(U[-2]) == dl
-            assert float(U[-1]) == (dl if eng is engine else 0.0)
+            assert float(U[-4]) == dl
+            assert float(U[-3]) == (dl if eng is engine else 0.0)
             acc += U
         sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
         sc = torch.empty(n, dtype=torch.float64, device="cuda")
@@ -226,8 +226,8 @@ def test_f32_mfma_record_carries_its_roundoff(engine, oracle):
         sq = oracle.sqnorms(X.cpu().numpy())
         GU.check_margin(mg, sc.cpu().numpy(), sq, n, f, d, u_gram=2.0 ** -24)
         # a record without a column count: unknown bound, always a near tie
-        acc[-2] = 0.0
-        acc[-1] = 0.0
+        acc[-4] = 0.0
+        acc[-3] = 0.0
         other.finish_ptr(acc.data_ptr(), X.data_ptr(), _lib.BK_F32, n, d, d, f, sel.data_ptr(),
                          sc.data_ptr(), None)
         mg0 = other.selection_margin()

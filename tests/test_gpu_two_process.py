@@ -72,7 +72,7 @@ def _worker(rank, world, port, names, q):
             parts = [None] * world
             dist.all_gather_object(parts, (c0, mean[:dl].cpu().numpy()))
             full_mean = np.concatenate([m for _, m in sorted(parts, key=lambda t: t[0])])
-            out[name] = (sel.cpu().numpy(), sc.cpu().numpy(), full_mean, mg, float(Uh[-2]))
+            out[name] = (sel.cpu().numpy(), sc.cpu().numpy(), full_mean, mg, float(Uh[-4]))
             del X, U
             torch.cuda.empty_cache()
         eng.close()

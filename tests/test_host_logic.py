@@ -28,7 +28,7 @@ def test_pack_unpack_roundtrip():
         G = A @ A.T
         U = D.pack_upper(G, 7)
         assert U.size == D.upper_elems(n)
-        assert U[-2] == 7.0 and U[-1] == 0.0
+        assert U[-4] == 7.0 and U[-3] == 0.0 and U[-2] == 0.0 and U[-1] == 0.0
         assert np.allclose(D.unpack_upper(U, n), G)
 
 
@@ -38,8 +38,9 @@ def test_packed_partials_sum_to_full_gram(oracle):
     parts = sum(D.pack_upper(oracle.gram(np.ascontiguousarray(X[:, c0:c0 + dl])), dl)
                 for c0, dl in D.all_shards(1000, 3))
     assert np.allclose(parts, full, rtol=1e-12, atol=1e-15)
-    assert parts[-2] == 1000.0  # the trailing pair sums to the total column count
-    assert parts[-1] == 0.0     # ... none of it on the fp32 MFMA
+    assert parts[-4] == 1000.0  # the trailing record sums to the total column count
+    assert parts[-3] == 0.0     # ... none of it on the fp32 MFMA
+    assert parts[-2] == 0.0     # ... nor int8-sliced
 
 
 def test_pack_upper_needs_a_column_count():
