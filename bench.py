@@ -165,7 +165,32 @@ def cpu_baseline(w, target_s=10.0, target_1core_s=6.0):
     return out
 
 
-F32_MODES = {"exact": 0, "mfma": 1, "certified": 2}  # bk_f32_mode
+F32_MODES = {"exact": 0, "mfma": 1, "certified": 2, "i8": 3, "i8_certified": 4}  # bk_f32_mode
+# int8 MFMA dense peak (MI355X: 2x the bf16 rate, ~5 POPS; measured 4.90 on
+# v_mfma_i32_32x32x32_i8, profiles/r01/ubench_i8.log)
+PEAK_I8_TOPS = 5000.0
+I8_PRODUCTS = 6  # K1i8's digit products of weight >= 2^-26 (bk_i8.hip)
+
+
+def gram_roofline(n, dl, k_ms, dtype, f32_mode, exact_rerun=False):
+    """The dominant kernel's roofline for the arithmetic it ran: fp64 MFMA
+    (fp64 rows, fp32 rows exact), fp32 MFMA (BK_F32_MFMA / CERTIFIED), int8
+    MFMA (BK_F32_I8*: 6 digit products per Gram element; achieved in int8
+    TOPS, plus the fp64-equivalent rate n(n+1) d / t)."""
+    flops = n * (n + 1) * dl
+    mode = "exact" if (dtype != "f32" or exact_rerun) else f32_mode
+    if mode in ("i8", "i8_certified"):
+        ops = I8_PRODUCTS * flops
+        ach = ops / (k_ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)",
+                "frac": round(ach / PEAK_I8_TOPS, 4), "ops_per_launch": ops,
+                "fp64_equiv_tflops": round(flops / (k_ms * 1e-3) / 1e12, 3),
+                "arithmetic": "int8 MFMA (6 exact digit products)"}
+    peak = PEAK_TFLOPS["f32" if mode in ("mfma", "certified") else "f64"]
+    ach = flops / (k_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "flops_per_launch": flops,
+            "arithmetic": "fp32 MFMA" if mode in ("mfma", "certified") else "fp64 MFMA"}
 
 
 def pmc_traffic(tag):
@@ -235,27 +260,39 @@ def device_variant(eng, dev, name, f32_mode="exact", steps=20, warmup=5, X=None)
         reruns = eng.certified_reruns() - r0
     finally:
         eng.set_f32_mode(0)
-    fp32_mma = w["dtype"] == "f32" and f32_mode != "exact" and reruns == 0
-    peak = PEAK_TFLOPS["f32" if fp32_mma else "f64"]
+    roof = gram_roofline(n, d, kt["avg_ms"], w["dtype"], f32_mode, exact_rerun=reruns > 0)
     flops = n * (n + 1) * d
-    ach = flops / (kt["avg_ms"] * 1e-3) / 1e12
+    peak = roof["peak"] if roof["unit"] == "TFLOP/s" else PEAK_TFLOPS["f64"]
     traffic, tsrc = pmc_traffic(workload_tag(name, f32_mode))
     bytes_alg = (n + m) * d * es + 8 * d
-    t_floor = max(flops / (peak * 1e12), bytes_alg / (PEAK_HBM_GBS * 1e9)) * 1e3
+    t_mx = (roof["ops_per_launch"] / (PEAK_I8_TOPS * 1e12) if "ops_per_launch" in roof
+            else flops / (peak * 1e12))
+    t_floor = max(t_mx, bytes_alg / (PEAK_HBM_GBS * 1e9)) * 1e3
     par = golden_check(name, sel.cpu().numpy(), mean.cpu().numpy(), 0, d) or {}
     par["margin"] = {"near_tie": mg["near_tie"], "gap": mg["gap"], "err_bound": mg["err_bound"]}
     out = {"n": n, "d": d, "f": f, "m": m, "dtype": w["dtype"], "f32_mode": f32_mode,
            "warmup": max(5, warmup), "steps": steps, "ms_per_step": round(ms, 4),
            "value": round(n * d * es / (ms * 1e-3) / 1e9, 3), "unit": "GB/s",
-           "roofline": {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                        "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": tsrc,
-                        "kernel": k1, "kernel_avg_ms": round(kt["avg_ms"], 4),
-                        "flops_per_launch": flops,
-                        "arithmetic": "fp32 MFMA" if fp32_mma else "fp64 MFMA"},
+           "roofline": dict(roof, traffic=traffic, traffic_source=tsrc, kernel=k1,
+                            kernel_avg_ms=round(kt["avg_ms"], 4)),
            "step_roofline": {"t_floor_ms": round(t_floor, 4), "frac": round(t_floor / ms, 4)},
            "parity": par}
-    if f32_mode == "certified":
+    if f32_mode in ("certified", "i8_certified"):
         out["certified_reruns"] = reruns
+    if f32_mode in ("i8", "i8_certified"):
+        kb = eng.timing_read()  # (cleared above) the slicing pass, evented once more
+        eng.timing_select(["k_slice", "k_reduce"])
+        eng.set_f32_mode(F32_MODES[f32_mode])
+        try:
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            kb = eng.timing_read()
+        finally:
+            eng.timing_select([])
+            eng.set_f32_mode(0)
+        out["k_slice_ms"] = round(kb.get("k_slice", {"avg_ms": float("nan")})["avg_ms"], 4)
+        out["k_reduce_ms"] = round(kb.get("k_reduce", {"avg_ms": float("nan")})["avg_ms"], 4)
     if traffic:
         out["roofline"]["traffic_ratio_to_unique_bytes"] = round(traffic / (n * d * es), 3)
     if own:
@@ -922,21 +959,18 @@ def main():
     k1name = "k_gram" if "k_gram" in kt else "k_small"
     g = kt.get(k1name, {"avg_ms": float("nan")})
     flops = n * (n + 1) * dl
-    achieved = flops / (g["avg_ms"] * 1e-3) / 1e12
     # fp64 rows and exact fp32 rows (widened) run the fp64 MFMA; BK_F32_MFMA /
-    # CERTIFIED the fp32 MFMA
-    fp32_mma = w["dtype"] == "f32" and a.f32_mode != "exact"
-    peak = PEAK_TFLOPS["f32" if fp32_mma else "f64"]
+    # CERTIFIED the fp32 MFMA; BK_F32_I8* the int8 MFMA
+    groof = gram_roofline(n, dl, g["avg_ms"], w["dtype"], a.f32_mode)
+    peak = groof["peak"] if groof["unit"] == "TFLOP/s" else PEAK_TFLOPS["f64"]
     # traffic: HBM bytes per K1 launch from the rocprofv3 PMC passes
     # (tools/profile.sh -> tools/pmc_summary.py), used only when that record was
     # taken with this very libbk.so build (sha256 prefix); otherwise null
     traffic, traffic_src = None, None
     if world == 1 and not emu:
         traffic, traffic_src = pmc_traffic(workload_tag(a.workload, a.f32_mode))
-    roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": k1name, "kernel_avg_ms": round(g["avg_ms"], 4),
-            "flops_per_launch": flops, "events_every": tstride}
+    roof = dict(groof, traffic=traffic, traffic_source=traffic_src, kernel=k1name,
+                kernel_avg_ms=round(g["avg_ms"], 4), events_every=tstride)
     if traffic:
         roof["traffic_ratio_to_unique_bytes"] = round(traffic / (n * dl * es), 3)
 
@@ -944,7 +978,8 @@ def main():
     # matrix peak, bytes_alg / HBM peak) with bytes_alg = (n + m) * d_local * s + 8 d_local;
     # and K4 (k_mean, the HBM-bound kernel) against HBM: m * d_local * s + 8 d_local bytes
     bytes_alg = (n + m) * dl * es + 8 * dl
-    t_mfma = flops / (peak * 1e12) * 1e3
+    t_mfma = (groof["ops_per_launch"] / (PEAK_I8_TOPS * 1e12) if "ops_per_launch" in groof
+              else flops / (peak * 1e12)) * 1e3
     t_hbm = bytes_alg / (PEAK_HBM_GBS * 1e9) * 1e3
     step_roof = {"t_floor_ms": round(max(t_mfma, t_hbm), 4),
                  "bound": "mfma" if t_mfma >= t_hbm else "hbm",
@@ -993,7 +1028,7 @@ def main():
                 "krum.go:100-166): the clock ramp a verifier sees",
         "ms": round(sc_step, 4), "GB_per_s": round(sc_gbs, 3),
         "k_gram_ms": round(sc_k1, 4),
-        "k_gram_frac": round(flops / (sc_k1 * 1e-3) / 1e12 / peak, 4) if sc_k1 > 0 else None,
+        "k_gram_frac": round(groof["frac"] * g["avg_ms"] / sc_k1, 4) if sc_k1 > 0 else None,
         "step_roofline_frac": round(max(t_mfma, t_hbm) / sc_step, 4),
         "calls_ms": [round(x, 4) for x in sc_all]}
 
@@ -1041,7 +1076,7 @@ def main():
                 XE = torch.empty((we["n"], we["d"]), dtype=torch.float32, device=dev)
                 eng.synth_fill_ptr(XE.data_ptr(), _lib.BK_F32, we["n"], we["d"], we["d"], 0,
                                    we["d"], we["seed"], we["nbyz"])
-            for mode in ("exact", "mfma", "certified"):
+            for mode in ("exact", "mfma", "certified", "i8", "i8_certified"):
                 if a.workload == "E_4096x262144_fp32" and mode == a.f32_mode:
                     continue  # that is the line itself
                 V[workload_tag("E_4096x262144_fp32", mode)] = device_variant(

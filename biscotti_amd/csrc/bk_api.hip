@@ -604,9 +604,12 @@ bool small_ok(const bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, 
 
 // margin_out / scores_out: the host entry's mapped output block (the record
 // and a second copy of the scores written by the kernel straight to host memory)
+// g0 / gn / sm: this launch's share -- the G items of chunks [g0, g0 + gn)
+// and, with sm, the S and M items (the pipelined host entry, below); the
+// default is the whole call in one launch
 int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld, int64_t f,
               int64_t *d_sel, double *d_scores, double *d_mean, double *margin_out = nullptr,
-              double *scores_out = nullptr) {
+              double *scores_out = nullptr, int g0 = 0, int gn = -1, bool sm = true) {
     const SmallPlan sp = small_plan((int)n, d, c->num_cu);
     if (!c->small_ctr.p) {
         CHK(ensure(c->small_ctr, SMALL_CTR_WORDS * sizeof(unsigned)));
@@ -624,7 +627,7 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
         sc = (double *)c->scores.p;
     }
     long long *trace = nullptr;
-    const int items = sp.ng + sp.Q + sp.nS + (d_mean ? sp.C : 1);
+    const int items = SMALL_SPLIT_ITEMS * (gn < 0 ? sp.P : gn) + (sm ? sp.nS + (d_mean ? sp.C : 1) : 0);
     const int grid = items < c->num_cu ? items : c->num_cu;  // = launch_small's grid
     const size_t twords = (size_t)items * 8 + (size_t)grid * 2;  // + per workgroup {entry, exit}
     const char *tfile = probe_env("BK_SMALL_TRACE");  // debug: per-item timeline
@@ -640,18 +643,20 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
                             (double *)c->U.p, sc, (double *)c->diag.p, d_sel, d_mean,
                             margin_out ? margin_out : c->dmargin,
                             (unsigned *)c->small_ctr.p, c->num_cu, c->stream, trace, spin,
-                            c->small_check_lines, scores_out);
+                            c->small_check_lines, scores_out, g0, gn, sm);
     }));
-    c->margin_valid = 1;
-    c->margin_host = margin_out ? c->hout_host_margin : c->hmargin;
-    c->margin_unchecked = 1;
+    if (sm) {
+        c->margin_valid = 1;
+        c->margin_host = margin_out ? c->hout_host_margin : c->hmargin;
+        c->margin_unchecked = 1;
+    }
     if (tfile) {
         std::vector<long long> h(twords + 6);
         h[0] = items;
-        h[1] = sp.ng;  // G items
+        h[1] = SMALL_SPLIT_ITEMS * (gn < 0 ? sp.P : gn);  // G items
         h[2] = sp.Q;
-        h[3] = sp.nS;
-        h[4] = d_mean ? sp.C : 1;
+        h[3] = sm ? sp.nS : 0;
+        h[4] = sm ? (d_mean ? sp.C : 1) : 0;
         h[5] = grid;
         HIPCHK(hipMemcpyAsync(h.data() + 6, trace, twords * sizeof(long long),
                               hipMemcpyDeviceToHost, c->stream));
@@ -746,6 +751,29 @@ struct HostDrain {
     }
 };
 
+// the host entries' copy stream and its five events, created once: into locals,
+// published together (a half-built set would break every later host call)
+int ensure_copy_stream(bk_ctx *c) {
+    if (c->copy) return BK_OK;
+    hipStream_t cs = nullptr;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+    for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        for (hipEvent_t x : ev)
+            if (x) (void)hipEventDestroy(x);
+        if (cs) (void)hipStreamDestroy(cs);
+        return fail(BK_EHIP, "copy stream / events: %s", hipGetErrorString(e));
+    }
+    c->copy = cs;
+    c->ev_go = ev[0];
+    c->ev_cp[0] = ev[1];
+    c->ev_cp[1] = ev[2];
+    c->ev_use[0] = ev[3];
+    c->ev_use[1] = ev[4];
+    return BK_OK;
+}
+
 // Host entries (bk_multikrum, bk_multikrum_noised): the batch crosses PCIe in
 // column chunks on a copy stream, and each chunk's partial Gram (K1 + K1b,
 // after K6 when noise is applied) runs on the compute stream while the next
@@ -759,27 +787,7 @@ int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const 
                          int64_t k, int64_t noise_ld, int64_t n, int64_t d, char *dX,
                          int64_t dld, double *U, Plan &pl) {
     const size_t es = esize(dtype);
-    if (!c->copy) {
-        // create the copy stream and its five events into locals and publish
-        // them together: a half-built set would break every later host call
-        hipStream_t cs = nullptr;
-        hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-        hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
-        for (int i = 0; i < 5 && e == hipSuccess; ++i)
-            e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
-        if (e != hipSuccess) {
-            for (hipEvent_t x : ev)
-                if (x) (void)hipEventDestroy(x);
-            if (cs) (void)hipStreamDestroy(cs);
-            return fail(BK_EHIP, "copy stream / events: %s", hipGetErrorString(e));
-        }
-        c->copy = cs;
-        c->ev_go = ev[0];
-        c->ev_cp[0] = ev[1];
-        c->ev_cp[1] = ev[2];
-        c->ev_use[0] = ev[3];
-        c->ev_use[1] = ev[4];
-    }
+    CHK(ensure_copy_stream(c));
     // chunks of ~BK_STAGE_CHUNK_BYTES (default 256 MiB) of the batch plus its
     // noise; widths a multiple of 64 columns (16-B aligned chunk starts)
     int64_t cap = (int64_t)256 << 20;
@@ -907,7 +915,44 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
             (void)hipGetLastError();  // not mapped (pinned by other means): copy it
         }
     }
-    if (where != BK_DEVICE && !zero_copy) {
+    // config B's verifier call (a host batch k_small takes, no noise): the copy
+    // in nc column chunks on the copy stream, each chunk's G items launched on
+    // the compute stream as soon as it has landed (an event, no spinning), so
+    // the Gram runs under the rest of the copy; then one S + M launch.  The
+    // same items and partials as the one-launch call: the same bits.
+    // BK_SMALL_PIPE=<chunks> (default 4; 0: one copy, then one launch)
+    static const int pipe_env = [] {
+        const char *e = getenv("BK_SMALL_PIPE");
+        return e ? atoi(e) : 4;
+    }();
+    const SmallPlan sp = small_plan((int)n, d, c->num_cu);
+    int nc = 0;
+    if (where != BK_DEVICE && !zero_copy && k == 0 && !noised_out && !tiny_ok((int)n, d) &&
+        !probe_env("BK_SMALL_TRACE") && pipe_env >= 2 && sp.P >= 2 * pipe_env)
+        nc = pipe_env;
+    if (nc) {
+        const int64_t epg = (int64_t)(16 / es);
+        dld = (d + epg - 1) / epg * epg;
+        CHK(ensure(c->X, (size_t)n * dld * es));
+        CHK(ensure_copy_stream(c));
+        char *dx = (char *)c->X.p;
+        // earlier work on the compute stream may still read the device batch
+        HIPCHK(hipEventRecord(c->ev_go, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->copy, c->ev_go, 0));
+        for (int q = 0; q < nc; ++q) {
+            const int a0 = (int)((int64_t)sp.P * q / nc), a1 = (int)((int64_t)sp.P * (q + 1) / nc);
+            const int64_t c0 = (int64_t)a0 * sp.kc, c1 = std::min<int64_t>((int64_t)a1 * sp.kc, d);
+            HIPCHK(hipMemcpy2DAsync(dx + c0 * es, (size_t)dld * es, (const char *)X + c0 * es,
+                                    (size_t)ld * es, (size_t)(c1 - c0) * es, (size_t)n,
+                                    hipMemcpyHostToDevice, c->copy));
+            HIPCHK(hipEventRecord(c->ev_cp[q & 1], c->copy));
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_cp[q & 1], 0));
+            CHK(run_small(c, dx, dtype, n, d, dld, f, nullptr, nullptr, nullptr, nullptr, nullptr,
+                          a0, a1 - a0, false));
+        }
+        dX = dx;
+    }
+    if (where != BK_DEVICE && !zero_copy && !nc) {
         const int64_t epg = (int64_t)(16 / es);
         dld = (d + epg - 1) / epg * epg;
         CHK(ensure(c->X, (size_t)n * dld * es));
@@ -983,7 +1028,7 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
     int64_t *dsel = (int64_t *)(blk + MPAD);
     double *dmean = mean_out ? blk + MPAD + 2 * n : nullptr;
     CHK(run_small(c, dX, dtype, n, d, dld, f, dsel, nullptr, dmean, blk,
-                  scores ? blk + MPAD + n : nullptr));
+                  scores ? blk + MPAD + n : nullptr, 0, nc ? 0 : -1, true));
     HIPCHK(wait_stream(c));
     drain.armed = false;
     const double *h = (const double *)c->hout;

@@ -201,6 +201,7 @@ struct SmallPlan {
 SmallPlan small_plan(int n, int64_t d, int num_cu);
 // n <= 16 and d <= 128 (config A): launch_small runs k_tiny, one workgroup
 bool tiny_ok(int n, int64_t d);
+constexpr int SMALL_SPLIT_ITEMS = 4;       // G items per chunk (bk_small.hip SMALL_SPLIT)
 constexpr int SMALL_CTR_WORDS = 71 * 32;  // 71 queue lines of 128 B (bk_small.hip)
 constexpr uint64_t SMALL_SPIN_MAX = 1ull << 24;  // polls before a hand-off wait gives up (~1 s)
 hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, int f,
@@ -208,7 +209,7 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
                         hipStream_t st, long long *trace = nullptr,
                         uint64_t spin_max = SMALL_SPIN_MAX, int check_lines = 0,
-                        double *scores_out = nullptr);
+                        double *scores_out = nullptr, int g0 = 0, int gn = -1, bool sm = true);
 hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, int64_t c0,
                         const int64_t *perm, const SynthParams &P, hipStream_t st);
 

@@ -63,7 +63,7 @@ static_assert(C_LINES * 32 == SMALL_CTR_WORDS, "bk_internal.h SMALL_CTR_WORDS");
 #endif
 constexpr int SMALL_KC = BK_SMALL_KC;  // columns per chunk (groups of 8)
 constexpr int SMALL_GR = SMALL_KC / 2;  // 16-B granules per staged row
-constexpr int SMALL_SPLIT = 4;          // G items per chunk (each: a quarter of the blocks)
+constexpr int SMALL_SPLIT = SMALL_SPLIT_ITEMS;  // G items per chunk (each: a quarter of the blocks)
 #ifndef BK_SMALL_NT
 #define BK_SMALL_NT 512
 #endif
@@ -93,6 +93,12 @@ struct SmallArgs {
     const void *X;
     int64_t ld, d;
     int n, f, kc, P, Q, nS, C, nblk, T;
+    // the launch's share (bk_multikrum's pipelined host entry, config B): the G
+    // items of chunks [g0, g0 + gn) and, with sm, the S and M items.  The
+    // one-launch call: g0 = 0, gn = P, sm = 1.  A G-only launch (sm = 0) hands
+    // its partials to the next launch on the stream by the kernel boundary; an
+    // S+M-only launch (gn = 0) finds every partial written
+    int g0, gn, sm;
     double *part, *U, *scores, *diag, *mean, *margin;
     double *scores_out;  // optional second copy of the scores (the host entry's mapped block)
     int64_t *sel;
@@ -424,7 +430,8 @@ template <typename T, bool VEC, int NB>
 __device__ __forceinline__ void small_gram(const SmallArgs &a, int it, int wave, int lane,
                                            char *tile, double *wb) {
     int c, h;
-    g_item(it, a.P, c, h);
+    g_item(it, a.gn, c, h);
+    c += a.g0;
     long long *tr = a.trace ? a.trace + 8 * (int64_t)it : nullptr;
     SmallStage<T, VEC, NB> st;
     st.load(a, c, lane + 64 * wave);
@@ -700,8 +707,8 @@ __global__ __launch_bounds__(SMALL_NT) void k_small(SmallArgs a) {
     __shared__ double wbuf[SMALL_NW][16 * 17];  // G: each wave's block on its way out
     static_assert(16 * NB * SMALL_GR * 16 >= 6 * 16 * NB * 8, "S items keep their sums in the tile");
     const int tid = threadIdx.x, wave = tid >> 6;
-    const int NGI = SMALL_SPLIT * a.P;  // G items: SPLIT per chunk
-    const int total = NGI + a.n + a.C;
+    const int NGI = SMALL_SPLIT * a.gn;  // G items: SPLIT per chunk of this launch
+    const int total = NGI + (a.sm ? a.n + a.C : 0);
     unsigned *ctr = a.ctr;
     // the first S0 items (G items) go to workgroups by blockIdx, the rest in
     // queue order (one returning atomic each): 256 dequeues on one counter
@@ -744,9 +751,10 @@ __global__ __launch_bounds__(SMALL_NT) void k_small(SmallArgs a) {
         }
         if (it < NGI) {
             small_gram<T, VEC, NB>(b, it, wave, olane, tile, &wbuf[wave][0]);
-            if (wg_arrive(ctr, C_G, G_GRP, it, NGI, &s_old)) wg_raise(ctr, F_G);
+            // (a G-only launch: the kernel boundary is the hand-off)
+            if (a.sm && wg_arrive(ctr, C_G, G_GRP, it, NGI, &s_old)) wg_raise(ctr, F_G);
         } else if (it < NGI + a.n) {
-            wg_wait_flag(ctr, F_G, a.spin_max);
+            if (NGI > 0) wg_wait_flag(ctr, F_G, a.spin_max);
             if (a.trace && tid == 0) a.trace[8 * it + 1] = (long long)__builtin_amdgcn_s_memrealtime();
             // the S item's chain sums and Gram row live in the (idle) G tile
             d2v *gv2 = reinterpret_cast<d2v *>(tile);
@@ -973,8 +981,11 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
                         const SmallPlan &p, double *part, double *U, double *scores, double *diag,
                         int64_t *sel, double *mean, double *margin, unsigned *ctr, int num_cu,
                         hipStream_t st, long long *trace, uint64_t spin_max, int check_lines,
-                        double *scores_out) {
+                        double *scores_out, int g0, int gn, bool sm) {
     SmallArgs a;
+    a.g0 = g0;
+    a.gn = gn < 0 ? p.P : gn;
+    a.sm = sm ? 1 : 0;
     a.scores_out = scores_out;
     a.trace = trace;
     a.spin_max = spin_max;
@@ -999,10 +1010,10 @@ hipError_t launch_small(const void *X, int dtype, int64_t ld, int n, int64_t d, 
     a.margin = margin;
     a.sel = sel;
     a.ctr = ctr;
-    const int total = SMALL_SPLIT * a.P + a.n + a.C;
+    const int total = SMALL_SPLIT * a.gn + (a.sm ? a.n + a.C : 0);
     const int grid = total < num_cu ? total : num_cu;
     const bool vec = (ld % 2) == 0 && ((uintptr_t)X % (dtype == 0 ? 16 : 8)) == 0;
-    if (tiny_ok(n, d) && !trace) {  // one workgroup, no hand-offs (k_tiny)
+    if (tiny_ok(n, d) && !trace && g0 == 0 && a.gn == p.P && sm) {  // one workgroup (k_tiny)
         if (scores_out) a.scores = scores_out;  // k_tiny never reads its scores back
         if (dtype == 0 && vec)
             hipLaunchKernelGGL((k_tiny<double, true>), dim3(1), dim3(256), 0, st, a);

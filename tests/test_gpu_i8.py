@@ -63,15 +63,18 @@ def _bound(X):
 
 
 @pytest.mark.parametrize("n,d", [(129, 64), (130, 4096), (256, 4160), (300, 20000), (512, 4000),
-                                 (1000, 777), (200, 70000)])
+                                 (1000, 780), (200, 70000)])
 def test_exact_on_scaled_small_integers(engine, n, d):
     rng = np.random.default_rng(n + d)
     X = rng.integers(-64, 65, size=(n, d)).astype(np.float32)
     X *= (2.0 ** rng.integers(-10, 11, size=(n, 1))).astype(np.float32)  # per-row scales
     X[3] = 0.0  # an all-zero row
+    from biscotti_amd.dist import unpack_upper
     want = _upper(engine, X, _lib.BK_F32_EXACT)
     got = _upper(engine, X, _lib.BK_F32_I8)
-    assert np.array_equal(got[:-4], want[:-4])  # the tiles, bit for bit
+    # the Gram, bit for bit (a diagonal sub-tile's lower half is not part of
+    # the packed contract: K1 leaves it, K1i8 writes it symmetric)
+    assert np.array_equal(unpack_upper(got, n), unpack_upper(want, n))
     assert got[-4] == d and got[-3] == 0.0 and got[-1] == 0.0
     assert got[-2] == pytest.approx(_bound(X), rel=1e-12)
 
@@ -173,6 +176,17 @@ def test_i8_margin_record(engine, oracle):
     X64 = X.astype(np.float64)
     scale = np.max(np.abs(X64[osel]).sum(0) / len(osel))
     assert np.max(np.abs(mean - omean)) <= 1e-9 * scale
+
+
+def test_unaligned_rows_take_the_exact_path(engine):
+    """K1i8 stages 16-B granules: rows with ld % 4 != 0 take the exact path
+    (its record carries no int8 bound) and return the exact Gram."""
+    from biscotti_amd.dist import unpack_upper
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((300, 777)).astype(np.float32)
+    want = _upper(engine, X, _lib.BK_F32_EXACT)
+    got = _upper(engine, X, _lib.BK_F32_I8)
+    assert got[-2] == 0.0 and np.array_equal(unpack_upper(got, 300), unpack_upper(want, 300))
 
 
 def test_i8_nonfinite_is_a_near_tie(engine):

@@ -202,3 +202,42 @@ def test_host_small_strided_view(engine, oracle, dtype, n, d, ld, f):
     assert np.max(np.abs(sc - osc)) <= 1e-9 * max(1e-300, np.max(np.abs(osc)))
     mscale = float(np.max(np.mean(np.abs(Xv[osel].astype(np.float64)), axis=0)))
     assert np.max(np.abs(mean - omean)) <= 1e-9 * max(mscale, 1e-300)
+
+
+@pytest.mark.parametrize("n,d,f,dtype,pad", [
+    (100, 7850, 30, np.float64, 0),   # config B (mnist): 62 chunks, 4 pipelined copies
+    (100, 7849, 30, np.float64, 1),   # odd d, padded host rows
+    (128, 2048, 60, np.float32, 0),   # the smallest pipelined batch (16 chunks)
+    (37, 30001, 11, np.float64, 0),
+    (64, 4099, 20, np.float32, 3)])
+def test_host_entry_pipelined_bitwise(engine, oracle, n, d, f, dtype, pad):
+    """bk_multikrum from a host batch (pinned and pageable)
+    copies it in column chunks on the copy stream and launches each chunk's G
+    items as soon as it lands, then one S + M launch: the same items and
+    partials as the device-resident one-launch call, so the selection, scores
+    and mean are bitwise the device call's."""
+    import ctypes
+    full = oracle.synth(n, d + pad, 4000 + n + d, f, dtype=dtype)
+    Xv = full[:, :d]
+    ref = _run(engine, torch.from_numpy(np.ascontiguousarray(Xv)).cuda(), f)
+    engine.timing_enable(True)
+    got = engine.multikrum(Xv, f)  # pageable
+    t = engine.timing_read()
+    engine.timing_enable(False)
+    assert t["k_small"]["count"] == 5 and "h2d" not in t, t  # 4 G launches + 1 S+M launch
+    for u, v in zip(got, ref):
+        assert np.array_equal(u.view(np.uint8), v.view(np.uint8))
+    # pinned (the verifier's stage_alloc buffers)
+    Xp = torch.from_numpy(np.ascontiguousarray(full)).pin_memory()
+    m = n - f
+    sel = np.empty(m, dtype=np.int64)
+    sc = np.empty(n, dtype=np.float64)
+    mean = np.empty(d, dtype=np.float64)
+    mo = ctypes.c_int64(0)
+    dt = _lib.BK_F32 if dtype == np.float32 else _lib.BK_F64
+    _lib.check(_lib.lib().bk_multikrum(engine.ctx, ctypes.c_void_p(Xp.data_ptr()),
+                                       _lib.BK_HOST_PINNED, dt, n, d, d + pad, f, sel.ctypes.data,
+                                       ctypes.addressof(mo), sc.ctypes.data, mean.ctypes.data))
+    for u, v in zip((sel, sc, mean), ref):
+        assert np.array_equal(u.view(np.uint8), v.view(np.uint8))
+    engine.selection_margin()  # the S + M launch's record is readable (no hand-off error)
