@@ -18,6 +18,7 @@ BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
 BK_ABI_VERSION = 10
 BK_F32_EXACT, BK_F32_MFMA, BK_F32_CERTIFIED, BK_F32_I8, BK_F32_I8_CERTIFIED = 0, 1, 2, 3, 4
+BK_F64_EXACT, BK_F64_I8, BK_F64_I8_CERTIFIED = 0, 3, 4
 KERNELS = ["k_gram", "k_reduce", "k_transpose", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni",
            "k_small", "k_slice"]
@@ -56,6 +57,7 @@ SIGNATURES = {
     "bk_timing_enable": (_i, [_p, _i]),
     "bk_graph_enable": (_i, [_p, _i]),
     "bk_set_f32_mode": (_i, [_p, _i]),
+    "bk_set_f64_mode": (_i, [_p, _i]),
     "bk_timing_select": (_i, [_p, ctypes.c_uint32]),
     "bk_timing_stride": (_i, [_p, ctypes.c_int]),
     "bk_timing_read": (_i, [_p, _i, _pd, _pi64]),

@@ -156,6 +156,7 @@ struct bk_ctx {
     int gram_variant = 3;  // 3: LDS-shared v3 for aligned fp64; 1: v1 everywhere (BK_GRAM=v1)
     int gram_mode = 0;     // BK_GRAM_MODE: timing-only ablations of v3 (tools/, never tests)
     int f32_mode = BK_F32_EXACT;  // fp32 rows: widened onto the fp64 MFMA, or the fp32 MFMA
+    int f64_mode = BK_F64_EXACT;  // fp64 rows: the fp64 MFMA, or K1i8 (bk_set_f64_mode)
     // hipGraph replay of bk_multikrum_device (bk_graph_enable): one captured
     // launch sequence per call signature; every workspace reallocation or plan
     // eviction bumps ws_epoch, which retires the graphs that baked the old
@@ -379,25 +380,27 @@ bool f32_mfma_now(const bk_ctx *c, int dtype) {
            (c->f32_mode == BK_F32_MFMA || c->f32_mode == BK_F32_CERTIFIED);
 }
 
-// fp32 rows on the int8-sliced Gram (K1i8) for this call: BK_F32_I8, or
-// BK_F32_I8_CERTIFIED outside its exact re-run; 16-B aligned rows, d >= 64
+// rows on the int8-sliced Gram (K1i8) for this call: fp32 rows under
+// BK_F32_I8 / BK_F32_I8_CERTIFIED, fp64 rows under BK_F64_I8 /
+// BK_F64_I8_CERTIFIED, outside a certified exact re-run; 16-B aligned rows, d >= 64
 bool i8_now(const bk_ctx *c, const void *dX, int dtype, int64_t d, int64_t ld) {
-    return dtype == BK_F32 && !c->force_exact && d >= 64 && (ld % 4) == 0 &&
-           ((uintptr_t)dX % 16) == 0 &&
-           (c->f32_mode == BK_F32_I8 || c->f32_mode == BK_F32_I8_CERTIFIED);
+    const int mode = dtype == BK_F32 ? c->f32_mode : c->f64_mode;
+    const int64_t epg = dtype == BK_F32 ? 4 : 2;
+    return !c->force_exact && d >= 64 && (ld % epg) == 0 && ((uintptr_t)dX % 16) == 0 &&
+           (mode == BK_F32_I8 || mode == BK_F32_I8_CERTIFIED);
 }
 
 // K1i8's layout (ranges, tile order) and its device tables, cached per (n, d)
-int get_i8(bk_ctx *c, int64_t n, int64_t d, bk_ctx::I8Cached **out) {
+int get_i8(bk_ctx *c, int64_t n, int64_t d, int es, bk_ctx::I8Cached **out) {
     for (auto &e : c->i8)
-        if (e.n == n && e.d == d) {
+        if (e.n == n && e.d == d && e.L.es == es) {
             *out = &e;
             return BK_OK;
         }
     bk_ctx::I8Cached e;
     e.n = n;
     e.d = d;
-    e.L = i8_layout((int)n, d);
+    e.L = i8_layout((int)n, d, es);
     const size_t tb = (size_t)(e.L.R + 1) * 8 + e.L.order.size() * sizeof(int);
     std::vector<char> h(tb);
     memcpy(h.data(), e.L.rb.data(), (size_t)(e.L.R + 1) * 8);
@@ -423,7 +426,7 @@ int get_i8(bk_ctx *c, int64_t n, int64_t d, bk_ctx::I8Cached **out) {
 int prepare_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld) {
     if (i8_now(c, dX, dtype, d, ld)) {
         bk_ctx::I8Cached *e = nullptr;
-        CHK(get_i8(c, n, d, &e));
+        CHK(get_i8(c, n, d, (int)esize(dtype), &e));
         return ensure(c->i8ws, i8_workspace(e->L));
     }
     if (use_v3(c, dX, dtype, ld)) {
@@ -454,7 +457,7 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
         // K1i8: digit slices + bound (k_slice), the int8 GEMM (k_gram), the
         // fixed-order sum of the range partials + the record (k_reduce)
         bk_ctx::I8Cached *e = nullptr;
-        CHK(get_i8(c, n, d, &e));
+        CHK(get_i8(c, n, d, (int)esize(dtype), &e));
         CHK(ensure(c->i8ws, i8_workspace(e->L)));
         pl.n = (int)n;
         pl.d = d;
@@ -463,7 +466,7 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
         const I8Layout &L = e->L;
         void *ws = c->i8ws.p, *tb = e->tables;
         CHK(timed(c, BK_K_SLICE, [&] {
-            return launch_i8_slice((const float *)dX, ld, (int)n, d, L, ws, tb, c->stream);
+            return launch_i8_slice(dX, dtype, ld, (int)n, d, L, ws, tb, c->stream);
         }));
         CHK(timed(c, BK_K_GRAM, [&] { return launch_i8_gemm((int)n, L, ws, tb, c->stream); }));
         CHK(timed(c, BK_K_REDUCE, [&] { return launch_i8_reduce(d, L, ws, U, c->stream); }));
@@ -1053,7 +1056,8 @@ struct DeviceGuard {
 };
 
 bool certified(const bk_ctx *c, int dtype) {
-    return dtype == BK_F32 && (c->f32_mode == BK_F32_CERTIFIED || c->f32_mode == BK_F32_I8_CERTIFIED);
+    if (dtype == BK_F64) return c->f64_mode == BK_F64_I8_CERTIFIED;
+    return c->f32_mode == BK_F32_CERTIFIED || c->f32_mode == BK_F32_I8_CERTIFIED;
 }
 
 // BK_F32_CERTIFIED: run on the fp32 MFMA; if the selection margin does not
@@ -1351,6 +1355,16 @@ int bk_set_f32_mode(bk_ctx *c, int mode) {
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f32_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
     c->f32_mode = mode;
+    return BK_OK;
+}
+
+int bk_set_f64_mode(bk_ctx *c, int mode) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    if (mode != BK_F64_EXACT && mode != BK_F64_I8 && mode != BK_F64_I8_CERTIFIED)
+        return fail(BK_EINVAL, "bad f64 mode %d", mode);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->f64_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
+    c->f64_mode = mode;
     return BK_OK;
 }
 

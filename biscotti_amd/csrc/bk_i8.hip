@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "bk_internal.h"
@@ -58,44 +59,51 @@ constexpr int I8_STAGE = 2 * I8_OPND;              // 48 KiB
 constexpr int I8_LDS = 2 * I8_STAGE;               // 96 KiB
 
 // ---------------------------------------------------------------------------
-// slicing: grid (npad rows, R ranges), 256 threads, 16 columns per thread-step
+// slicing: grid (npad rows, R ranges), 256 threads.  The range's row slice
+// (<= 128 KiB: R is chosen for it, i8_layout) is read ONCE from HBM into LDS
+// with 16-B loads while its max |x| and ||x||_1 accumulate, then the digits
+// are cut from LDS, 16 columns per thread-step, three 16-B stores each.
+// T = float (config E) or double (fp64 rows: the same digits, every step
+// exact in fp64 too; only the remainder past the third digit is dropped)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_i8_slice(const float *__restrict__ X, int64_t ld, int n,
+template <typename T>
+__global__ __launch_bounds__(256) void k_i8_slice(const T *__restrict__ X, int64_t ld, int n,
                                                   int64_t d, const int64_t *__restrict__ rb, int R,
                                                   int8_t *__restrict__ S, int64_t dp, int64_t plane,
                                                   int *__restrict__ es, double *__restrict__ l1o) {
-    __shared__ float smx[4];
-    __shared__ double sl1[4];
+    extern __shared__ __attribute__((aligned(16))) char slab[];
+    T *xs = reinterpret_cast<T *>(slab);
+    __shared__ double smx[4], sl1[4];
     __shared__ int sfin[4];
+    constexpr int EPG = 16 / sizeof(T);  // elements per 16-B granule
+    typedef T gvec __attribute__((ext_vector_type(EPG)));
     const int i = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
     const int64_t c0 = rb[r], c1 = rb[r + 1];
     const int64_t ce = c1 < d ? c1 : d;  // columns past d are zero
-    const float *xr = X + (int64_t)i * ld;
-    float mx = 0.0f;
-    double l1 = 0.0;
+    const int len = (int)(c1 - c0);      // a multiple of 64
+    const T *xr = X + (int64_t)i * ld + c0;
+    double mx = 0.0, l1 = 0.0;
     int fin = 1;
-    if (i < n) {
-        for (int64_t c = c0 + (int64_t)tid * 4; c < ce; c += 1024) {
-            float v[4];
-            if (c + 4 <= ce) {
-                const float4 q = *reinterpret_cast<const float4 *>(xr + c);
-                v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
-            } else {
+    for (int c = tid * EPG; c < len; c += 256 * EPG) {
+        gvec v;
+        if (i < n && c0 + c + EPG <= ce) {
+            v = *reinterpret_cast<const gvec *>(xr + c);
+        } else {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = c + u < ce ? xr[c + u] : 0.0f;
-            }
+            for (int u = 0; u < EPG; ++u) v[u] = (i < n && c0 + c + u < ce) ? xr[c + u] : (T)0;
+        }
+        *reinterpret_cast<gvec *>(xs + c) = v;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float a = __builtin_fabsf(v[u]);
-                fin &= a <= 3.4028235e38f;  // NaN and +-inf fail
-                mx = a > mx ? a : mx;
-                l1 += (double)a;
-            }
+        for (int u = 0; u < EPG; ++u) {
+            const double a = __builtin_fabs((double)v[u]);
+            fin &= a <= 1.7976931348623157e308;  // NaN and +-inf fail
+            mx = a > mx ? a : mx;
+            l1 += a;
         }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const float m2 = __shfl_xor(mx, o);
+        const double m2 = __shfl_xor(mx, o);
         mx = m2 > mx ? m2 : mx;
         l1 += __shfl_xor(l1, o);
         fin &= __shfl_xor(fin, o);
@@ -116,29 +124,21 @@ __global__ __launch_bounds__(256) void k_i8_slice(const float *__restrict__ X, i
     }
     // s = 2^e > max |x| (frexp: mx = m 2^e, m in [0.5, 1)); all-zero rows: e = 0
     int e = 0;
-    if (fin && mx > 0.0f) (void)frexpf(mx, &e);
+    if (fin && mx > 0.0) (void)frexp(mx, &e);
     if (tid == 0) {
         es[(int64_t)i * R + r] = e;
         l1o[(int64_t)i * R + r] = fin ? l1 : __builtin_inf();
     }
-    int8_t *s0 = S + (int64_t)i * dp, *s1 = s0 + plane, *s2 = s1 + plane;
-    for (int64_t c = c0 + (int64_t)tid * 16; c < c1; c += 4096) {
+    int8_t *s0 = S + (int64_t)i * dp + c0, *s1 = s0 + plane, *s2 = s1 + plane;
+    for (int c = tid * 16; c < len; c += 4096) {
         int dig[3][4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            float v[4];
-            const int64_t cc = c + 4 * q;
-            if (i < n && fin && cc + 4 <= ce) {
-                const float4 f = *reinterpret_cast<const float4 *>(xr + cc);
-                v[0] = f.x, v[1] = f.y, v[2] = f.z, v[3] = f.w;
-            } else {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = (i < n && fin && cc + u < ce) ? xr[cc + u] : 0.0f;
-            }
             int p0 = 0, p1 = 0, p2 = 0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const double y = ldexp((double)v[u], 6 - e);  // 64 x / s, exact
+                const double x = fin ? (double)xs[c + 4 * q + u] : 0.0;
+                const double y = ldexp(x, 6 - e);  // 64 x / s, exact
                 const double a0 = __builtin_rint(y);
                 const double y1 = (y - a0) * 128.0;  // exact
                 const double a1 = __builtin_rint(y1);
@@ -340,12 +340,21 @@ __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ pa
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-I8Layout i8_layout(int n, int64_t d) {
+// R column ranges: at least one per XCD, and as many more (in eights) as keep
+// a row's slice of a range within 128 KiB, so k_i8_slice reads it once into
+// LDS (config E, fp32: 8 ranges of 32,768 columns; config D, fp64: 64 of
+// 16,384); <= 32,768 columns per range keeps every int32 sum exact
+constexpr int64_t I8_RANGE_BYTES = 131072;
+I8Layout i8_layout(int n, int64_t d, int es) {
     I8Layout L;
     L.npad = (n + I8_TILE - 1) / I8_TILE * I8_TILE;
     L.dp = (d + I8_KC - 1) / I8_KC * I8_KC;
     const int64_t nk = L.dp / I8_KC;
-    L.R = (int)(nk < 8 ? nk : 8);
+    const int64_t cmax = I8_RANGE_BYTES / es;  // columns per range
+    int64_t R = (L.dp + cmax - 1) / cmax;
+    R = (R + 7) / 8 * 8;
+    L.R = (int)(nk < R ? nk : R);
+    L.es = es;
     L.rb.resize(L.R + 1);
     for (int r = 0; r <= L.R; ++r) L.rb[r] = nk * r / L.R * I8_KC;
     L.plane = (int64_t)L.npad * L.dp;
@@ -376,8 +385,15 @@ size_t i8_workspace(const I8Layout &L) {
 }
 
 hipError_t configure_i8_kernels() {
-    return hipFuncSetAttribute((const void *)k_gram_i8, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               I8_LDS);
+    hipError_t e = hipFuncSetAttribute((const void *)k_gram_i8,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, I8_LDS);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void *)k_i8_slice<float>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)I8_RANGE_BYTES);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void *)k_i8_slice<double>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)I8_RANGE_BYTES);
+    return e;
 }
 
 static char *align256(char *p) { return (char *)(((uintptr_t)p + 255) & ~(uintptr_t)255); }
@@ -403,12 +419,19 @@ static I8Ws i8_ws(const I8Layout &L, void *ws) {
     return w;
 }
 
-hipError_t launch_i8_slice(const float *X, int64_t ld, int n, int64_t d, const I8Layout &L,
-                           void *ws, const void *tables, hipStream_t st) {
+hipError_t launch_i8_slice(const void *X, int dtype, int64_t ld, int n, int64_t d,
+                           const I8Layout &L, void *ws, const void *tables, hipStream_t st) {
     const I8Ws w = i8_ws(L, ws);
     const int64_t *rb = (const int64_t *)tables;
-    hipLaunchKernelGGL(k_i8_slice, dim3((unsigned)L.npad, (unsigned)L.R), dim3(256), 0, st, X, ld, n,
-                       d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+    int64_t lmax = 0;  // the longest range (LDS bytes of its row slice)
+    for (int r = 0; r < L.R; ++r) lmax = std::max<int64_t>(lmax, L.rb[r + 1] - L.rb[r]);
+    const size_t lds = (size_t)lmax * L.es;
+    if (dtype == 0)
+        hipLaunchKernelGGL(k_i8_slice<double>, dim3((unsigned)L.npad, (unsigned)L.R), dim3(256), lds,
+                           st, (const double *)X, ld, n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+    else
+        hipLaunchKernelGGL(k_i8_slice<float>, dim3((unsigned)L.npad, (unsigned)L.R), dim3(256), lds,
+                           st, (const float *)X, ld, n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_i8_bound, dim3(1), dim3(256), 0, st, w.es, w.l1, rb, L.R, n, d, w.bound);

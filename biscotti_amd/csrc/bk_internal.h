@@ -177,20 +177,20 @@ hipError_t launch_roni_softmax_batches(const float *Xv, int64_t nv, int64_t din,
 // bk_i8.hip: K1i8, the Gram of fp32 rows from exact int8 digit slices
 // (BK_F32_I8): column ranges (one per XCD), digit planes [3][npad][dp] int8
 struct I8Layout {
-    int npad = 0, R = 0, T128 = 0, T64 = 0;
+    int npad = 0, R = 0, T128 = 0, T64 = 0, es = 4;
     int64_t dp = 0, plane = 0, ntile64 = 0;
     std::vector<int64_t> rb;  // range boundaries (R + 1, multiples of 64 columns)
     std::vector<int> order;   // the 128-row tiles (I <= J), super-blocked: pairs
 };
-I8Layout i8_layout(int n, int64_t d);
+I8Layout i8_layout(int n, int64_t d, int es);
 size_t i8_workspace(const I8Layout &L);
 hipError_t configure_i8_kernels();
 // tables: device copy of {rb (R + 1 int64), order (int pairs)}; ws:
 // i8_workspace(L) bytes.  slice: digit planes + the error bound; gemm: the
 // range partials; reduce: U (bk_upper_elems(n)) with the trailing record
 // {d, 0, bound, 0}
-hipError_t launch_i8_slice(const float *X, int64_t ld, int n, int64_t d, const I8Layout &L,
-                           void *ws, const void *tables, hipStream_t st);
+hipError_t launch_i8_slice(const void *X, int dtype, int64_t ld, int n, int64_t d,
+                           const I8Layout &L, void *ws, const void *tables, hipStream_t st);
 hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables, hipStream_t st);
 hipError_t launch_i8_reduce(int64_t d, const I8Layout &L, void *ws, double *U, hipStream_t st);
 

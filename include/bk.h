@@ -166,6 +166,15 @@ enum bk_f32_mode {
  * group's contexts (bk_group_ctx): a near tie re-runs every device's shard
  * exact from device memory, then exchanges and finishes again. */
 int bk_set_f32_mode(bk_ctx *ctx, int mode);
+/* fp64 rows (dtype BK_F64): BK_F64_EXACT (default) runs the fp64 MFMA;
+ * BK_F64_I8 takes the Gram from the same exact int8 digit slices as BK_F32_I8
+ * (the digits of an fp64 row: every slicing step exact, only the remainder
+ * past the third digit dropped) under the same absolute error bound;
+ * BK_F64_I8_CERTIFIED re-runs the fp64 MFMA on a near tie, so its selected
+ * set is always the reference's.  The mean is unchanged (K4 reads the fp64
+ * rows).  Rows must be 16-B aligned (even ld) and d >= 64. */
+enum bk_f64_mode { BK_F64_EXACT = 0, BK_F64_I8 = 3, BK_F64_I8_CERTIFIED = 4 };
+int bk_set_f64_mode(bk_ctx *ctx, int mode);
 /* BK_F32_I8_CERTIFIED: the same contract on the int8-sliced Gram.
  * exact re-runs BK_F32_CERTIFIED / BK_F32_I8_CERTIFIED have made on this context */
 int64_t bk_certified_reruns(bk_ctx *ctx);

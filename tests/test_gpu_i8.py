@@ -40,18 +40,24 @@ def _upper(engine, X, mode):
     return U.cpu().numpy()
 
 
-def _ranges(d):
+def _ranges(d, es):
+    """bk_i8.hip i8_layout: R column ranges of whole 64-column granules, at
+    least 8, in eights, each row slice <= 128 KiB."""
     dp = (d + 63) // 64 * 64
     nk = dp // 64
-    R = min(nk, 8)
+    cmax = 131072 // es
+    R = -(-dp // cmax)
+    R = -(-R // 8) * 8
+    R = min(nk, R)
     return [(nk * r // R * 64, nk * (r + 1) // R * 64) for r in range(R)]
 
 
 def _bound(X):
     """bk_i8.hip's absolute bound, restated from its definition."""
+    es = X.dtype.itemsize
     X = X.astype(np.float64)
     tot = 0.0
-    for c0, c1 in _ranges(X.shape[1]):
+    for c0, c1 in _ranges(X.shape[1], es):
         A = np.abs(X[:, c0:min(c1, X.shape[1])])
         if A.shape[1] == 0:
             continue
@@ -237,3 +243,76 @@ def test_i8_shard_records_sum(engine):
     assert mg["d"] == d
     want = GU.margin_bound(mg["M"], d, n - f - 2, eg=sum(bounds))
     assert abs(mg["err_bound"] - want) <= 1e-12 * want
+
+
+@pytest.mark.parametrize("name", [k for k in ("C_1024x131072", "D_512x1M_f153", "C_tight", "B_tight",
+                                               "n1000_d2000") if GU.have(k)])
+def test_f64_i8_matches_or_flags(name, engine, oracle):
+    """fp64 rows on K1i8 (bk_set_f64_mode): the selection equals the
+    reference's or is flagged; BK_F64_I8_CERTIFIED always returns the
+    reference's set, and the mean (K4 on the fp64 rows) within the §8(d) bound."""
+    p = GU.C.case_params(name)
+    n, d, f = p["n"], p["d"], p["f"]
+    if p["dtype"] != "float64":
+        pytest.skip("fp64 cases only")
+    X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, p["seed"], p["nbyz"],
+                          p["mu_scale"], p["byz_scale"], p["sigma"], p["flags"])
+    g = GU.load(name)
+    dev_run = lambda: _run64(engine, X, f)
+    try:
+        engine.set_f64_mode(_lib.BK_F64_I8)
+        sel, sc, mean = dev_run()
+        mg = engine.selection_margin()
+        if n > 128:  # n <= 128 takes k_small, always exact
+            assert mg["err_bound"] > 0
+        if not np.array_equal(sel, g["sel"]):
+            assert mg["near_tie"] and not mg["gap"] > mg["err_bound"], mg
+        err = float(np.max(np.abs(sc - g["scores"])))
+        print("%s fp64 K1i8: max score error %.3e, err_bound %.3e, gap %.3e, near_tie %s"
+              % (name, err, mg["err_bound"], mg["gap"], mg["near_tie"]))
+        assert err <= mg["err_bound"] / 2 + 1e-9 * float(np.max(np.abs(g["scores"])))
+        engine.set_f64_mode(_lib.BK_F64_I8_CERTIFIED)
+        sel2, _, mean2 = dev_run()
+        assert np.array_equal(sel2, g["sel"])
+        GU.check_mean(mean2, g, GU.manifest()[name])
+    finally:
+        engine.set_f64_mode(_lib.BK_F64_EXACT)
+    del X
+    torch.cuda.empty_cache()
+
+
+def _run64(engine, X, f):
+    n, d = X.shape
+    sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+    sc = torch.empty(n, dtype=torch.float64, device="cuda")
+    mean = torch.empty(d, dtype=torch.float64, device="cuda")
+    engine.multikrum_device_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr(),
+                                sc.data_ptr(), mean.data_ptr())
+    engine.synchronize()
+    return sel.cpu().numpy(), sc.cpu().numpy(), mean.cpu().numpy()
+
+
+@pytest.mark.parametrize("n,d", [(130, 4096), (300, 20000), (512, 70000)])
+def test_f64_i8_error_within_the_bound(engine, n, d):
+    from biscotti_amd.dist import unpack_upper
+    rng = np.random.default_rng(d + 1)
+    X = rng.standard_normal((n, d))
+    X[: n // 3] *= 1e-4
+    tX = torch.from_numpy(X).cuda()
+    usz = int(_lib.lib().bk_upper_elems(n))
+    out = {}
+    for mode in (_lib.BK_F64_EXACT, _lib.BK_F64_I8):
+        U = torch.empty(usz, dtype=torch.float64, device="cuda")
+        engine.set_f64_mode(mode)
+        try:
+            engine.gram_upper_ptr(tX.data_ptr(), _lib.BK_F64, n, d, d, U.data_ptr())
+            engine.synchronize()
+        finally:
+            engine.set_f64_mode(_lib.BK_F64_EXACT)
+        out[mode] = U.cpu().numpy()
+    E = float(out[_lib.BK_F64_I8][-2])
+    assert E == pytest.approx(_bound(X), rel=1e-12)
+    err = float(np.max(np.abs(unpack_upper(out[_lib.BK_F64_I8], n) - unpack_upper(out[_lib.BK_F64_EXACT], n))))
+    print("fp64 K1i8 n=%d d=%d: max err %.3e bound %.3e" % (n, d, err, E))
+    assert err <= E
