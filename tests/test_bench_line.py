@@ -1,0 +1,60 @@
+"""CPU: bench.py's printed line: the contract's keys, and
+as the LAST key a per-config summary small enough for the driver's stored
+tail; the full record goes to the detail file."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _record():
+    roof = {"bound": "mfma", "achieved": 68.0, "peak": 78.6, "unit": "TFLOP/s", "frac": 0.865,
+            "traffic": 1.07e10, "traffic_source": "x", "kernel": "k_gram", "kernel_avg_ms": 4.05,
+            "traffic_ratio_to_unique_bytes": 2.5}
+    par = {"selected_set": "match", "mean": "match",
+           "margin": {"near_tie": False, "gap": 5e5, "err_bound": 1e-3}}
+    dv = {"value": 1.0, "ms_per_step": 2.0, "roofline": roof, "parity": par, "steps": 20,
+          "step_roofline": {"t_floor_ms": 1.0, "frac": 0.5}, "filler": "x" * 4000}
+    sm = {"one_launch": {"ms_per_step": 0.02, "GB_per_s": 290.0, "parity": par}, "value": 290.0,
+          "ms_per_step": 0.02, "roofline": dict(roof, unit="GB/s"),
+          "host_entry": {"ms_per_call": 0.15, "overhead_over_h2d_ms": 0.02, "parity": par}}
+    variants = {k: dict(dv) for k in ("D_512x1M_f256", "C_1024x131072", "E_4096x262144_fp32",
+                                      "E_4096x262144_fp32_mfma", "E_4096x262144_fp32_certified",
+                                      "E_4096x262144_fp32_i8", "E_4096x262144_fp32_i8_certified",
+                                      "D_512x1M_f153_i8_certified")}
+    variants["E_4096x262144_fp32_i8_certified"]["certified_reruns"] = 0
+    variants["B_mnist"] = sm
+    variants["A_creditcard"] = sm
+    return {"metric": "m", "value": 940.0, "unit": "GB/s", "n_gpus": 1, "steps": 40, "warmup": 10,
+            "ms_per_step": 4.57, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic", "config": {"workload": "D_512x1M_f153"},
+            "roofline": roof, "roofline_hbm_k4": {"frac": 0.8}, "step_roofline": {"frac": 0.76},
+            "kernels_ms_avg": {"k_gram": 4.05}, "parity": par, "variants": variants,
+            "single_call": {"ms": 5.7, "k_gram_frac": 0.68},
+            "next_rows": {"k_noise": {"ms": 0.74, "roofline": {"frac": 0.72}}},
+            "e2e_pinned_h2d_d2h": {"GB_per_s": 56.0, "ms": 76.7},
+            "cpu_baseline": {"value": 2.4, "unit": "GB/s", "cores": 16, "kind": "port",
+                             "sample": "s", "value_1core": 0.18}}
+
+
+def test_compact_line_keeps_every_config_and_fits(tmp_path):
+    sys.path.insert(0, REPO)
+    import bench
+    rec = _record()
+    path = str(tmp_path / "detail.json")
+    line = bench.compact_line(rec, path)
+    s = json.dumps(line)
+    assert len(s) < 6000, len(s)
+    assert list(line)[-1] == "summary"
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in line, k
+    summ = line["summary"]
+    for k in list(rec["variants"]) + ["D_512x1M_f153"]:
+        assert k in summ and summ[k]["sel"] == "match", k
+        assert summ[k]["value"] is not None and summ[k]["ms"] is not None, k
+    assert summ["B_mnist"]["host_over_h2d_ms"] == 0.02
+    assert summ["E_4096x262144_fp32_i8_certified"]["reruns"] == 0
+    assert json.load(open(path))["variants"]["C_1024x131072"]["filler"]  # the full record

@@ -20,7 +20,7 @@ import sys
 
 # coalesced streaming readers (128-B requests tallied at 64 B): 16 B/lane, and
 # k_qsum's 8 B/lane (calibrated: doubled it equals m*d*8 exactly)
-WIDE_READS = ("k_gram3", "k_mean", "k_gram<", "k_noise", "k_qsum", "k_small")
+WIDE_READS = ("k_gram3", "k_mean", "k_gram<", "k_noise", "k_qsum", "k_small", "k_gram_i8", "k_i8_slice")
 # the roofline kernel: K1, or the one-launch path for n <= 128 (configs A, B)
 K1_NAMES = ("k_gram", "k_small", "k_tiny")
 
