@@ -80,8 +80,9 @@ def test_verifier_flow_against_oracle(harness, oracle, tmp_path):
             assert it["k_small"] == it["k_gram"] == 0
         else:
             assert it["status"] == 0
-            # the host entry took the one-launch path (k_small / k_tiny), never K1
-            assert (it["k_small"], it["k_gram"]) == (1, 0), it
+            # the host entry took the k_small / k_tiny path, never K1 (one
+            # launch, or the pipelined host entry's G launches + one S+M launch)
+            assert it["k_small"] >= 1 and it["k_gram"] == 0, it
             Xb = X[[sid_row[s] for s in it["batch"]]]
             osel, _, _ = oracle.krum(Xb, it["f"])
             assert it["accepted"] == [it["batch"][i] for i in osel], (k, it)
