@@ -56,51 +56,74 @@ constexpr int I8_TILE = 128, I8_KC = 64, I8_S = 3;
 constexpr int I8_PLANE = I8_TILE * I8_KC;          // one digit plane of one operand per stage: 8 KiB
 constexpr int I8_OPND = I8_S * I8_PLANE;           // 24 KiB
 constexpr int I8_STAGE = 2 * I8_OPND;              // 48 KiB
-constexpr int I8_LDS = 2 * I8_STAGE;               // 96 KiB
+// K1i8's operand pipeline (BK_I8_PIPE; A/B builds): 1 = LDS stores from
+// registers fetched one chunk ahead (2 stages), 3 = LDS-DMA (global_load_lds)
+// into a 3-stage ring, two chunks ahead.  (2, the register path two chunks
+// ahead, needs a second 48-register set: it spilled.)
+#ifndef BK_I8_PIPE
+#define BK_I8_PIPE 1
+#endif
+constexpr int I8_NSTAGE = BK_I8_PIPE == 3 ? 3 : 2;
+constexpr int I8_LDS = I8_NSTAGE * I8_STAGE;       // 96 / 144 KiB
+constexpr int I8_RANGE_BYTES = 131072;             // a row's slice of one column range (i8_layout)
 
 // ---------------------------------------------------------------------------
-// slicing: grid (npad rows, R ranges), 256 threads.  The range's row slice
-// (<= 128 KiB: R is chosen for it, i8_layout) is read ONCE from HBM into LDS
-// with 16-B loads while its max |x| and ||x||_1 accumulate, then the digits
-// are cut from LDS, 16 columns per thread-step, three 16-B stores each.
+// slicing: grid (npad rows, R ranges), 512 threads.  The range's row slice
+// (<= 128 KiB: R is chosen for it, i8_layout) is read ONCE from HBM straight
+// into registers -- thread t holds 16 consecutive columns of each 8,192-column
+// block, every load issued before the first is used -- while its max |x| and
+// ||x||_1 accumulate; then the digits are cut from the registers, three 16-B
+// stores per 16 columns.  (r4a staged the slice through 128 KiB of LDS: one
+// workgroup per CU, its loads in dependent rounds: 4.4 ms at config E.)
 // T = float (config E) or double (fp64 rows: the same digits, every step
 // exact in fp64 too; only the remainder past the third digit is dropped)
 // ---------------------------------------------------------------------------
+constexpr int I8_SLICE_NT = 512;
 template <typename T>
-__global__ __launch_bounds__(256) void k_i8_slice(const T *__restrict__ X, int64_t ld, int n,
-                                                  int64_t d, const int64_t *__restrict__ rb, int R,
-                                                  int8_t *__restrict__ S, int64_t dp, int64_t plane,
-                                                  int *__restrict__ es, double *__restrict__ l1o) {
-    extern __shared__ __attribute__((aligned(16))) char slab[];
-    T *xs = reinterpret_cast<T *>(slab);
-    __shared__ double smx[4], sl1[4];
-    __shared__ int sfin[4];
-    constexpr int EPG = 16 / sizeof(T);  // elements per 16-B granule
+__global__ __launch_bounds__(I8_SLICE_NT) void k_i8_slice(const T *__restrict__ X, int64_t ld, int n,
+                                                          int64_t d, const int64_t *__restrict__ rb,
+                                                          int R, int8_t *__restrict__ S, int64_t dp,
+                                                          int64_t plane, int *__restrict__ es,
+                                                          double *__restrict__ l1o) {
+    constexpr int EPG = 16 / sizeof(T);                               // elements per 16-B load
+    constexpr int BLK = 16 * I8_SLICE_NT;                             // columns per block
+    constexpr int MAXU = I8_RANGE_BYTES / (int)(sizeof(T) * BLK);     // blocks per range
+    static_assert(MAXU >= 1 && MAXU * BLK * (int)sizeof(T) == I8_RANGE_BYTES, "range blocks");
     typedef T gvec __attribute__((ext_vector_type(EPG)));
+    __shared__ double smx[I8_SLICE_NT / 64], sl1[I8_SLICE_NT / 64];
+    __shared__ int sfin[I8_SLICE_NT / 64];
     const int i = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
     const int64_t c0 = rb[r], c1 = rb[r + 1];
     const int64_t ce = c1 < d ? c1 : d;  // columns past d are zero
-    const int len = (int)(c1 - c0);      // a multiple of 64
-    const T *xr = X + (int64_t)i * ld + c0;
-    double mx = 0.0, l1 = 0.0;
-    int fin = 1;
-    for (int c = tid * EPG; c < len; c += 256 * EPG) {
-        gvec v;
-        if (i < n && c0 + c + EPG <= ce) {
-            v = *reinterpret_cast<const gvec *>(xr + c);
+    const int len = (int)(c1 - c0);      // a multiple of 64, <= MAXU * BLK
+    const T *xr = X + (int64_t)(i < n ? i : 0) * ld + c0;
+    T v[MAXU][16];
+#pragma unroll
+    for (int u = 0; u < MAXU; ++u) {
+        const int c = u * BLK + 16 * tid;
+        if (i < n && c0 + c + 16 <= ce) {
+#pragma unroll
+            for (int q = 0; q < 16 / EPG; ++q) {
+                const gvec g = *reinterpret_cast<const gvec *>(xr + c + EPG * q);
+#pragma unroll
+                for (int e = 0; e < EPG; ++e) v[u][EPG * q + e] = g[e];
+            }
         } else {
 #pragma unroll
-            for (int u = 0; u < EPG; ++u) v[u] = (i < n && c0 + c + u < ce) ? xr[c + u] : (T)0;
+            for (int e = 0; e < 16; ++e) v[u][e] = (i < n && c < len && c0 + c + e < ce) ? xr[c + e] : (T)0;
         }
-        *reinterpret_cast<gvec *>(xs + c) = v;
+    }
+    double mx = 0.0, l1 = 0.0;
+    int fin = 1;
 #pragma unroll
-        for (int u = 0; u < EPG; ++u) {
-            const double a = __builtin_fabs((double)v[u]);
+    for (int u = 0; u < MAXU; ++u)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const double a = __builtin_fabs((double)v[u][e]);
             fin &= a <= 1.7976931348623157e308;  // NaN and +-inf fail
             mx = a > mx ? a : mx;
             l1 += a;
         }
-    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const double m2 = __shfl_xor(mx, o);
@@ -117,7 +140,8 @@ __global__ __launch_bounds__(256) void k_i8_slice(const T *__restrict__ X, int64
     mx = smx[0];
     l1 = sl1[0];
     fin = sfin[0];
-    for (int w = 1; w < 4; ++w) {
+#pragma unroll
+    for (int w = 1; w < I8_SLICE_NT / 64; ++w) {
         mx = smx[w] > mx ? smx[w] : mx;
         l1 += sl1[w];
         fin &= sfin[w];
@@ -130,22 +154,25 @@ __global__ __launch_bounds__(256) void k_i8_slice(const T *__restrict__ X, int64
         l1o[(int64_t)i * R + r] = fin ? l1 : __builtin_inf();
     }
     int8_t *s0 = S + (int64_t)i * dp + c0, *s1 = s0 + plane, *s2 = s1 + plane;
-    for (int c = tid * 16; c < len; c += 4096) {
+#pragma unroll
+    for (int u = 0; u < MAXU; ++u) {
+        const int c = u * BLK + 16 * tid;
+        if (c >= len) continue;
         int dig[3][4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             int p0 = 0, p1 = 0, p2 = 0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const double x = fin ? (double)xs[c + 4 * q + u] : 0.0;
+            for (int w = 0; w < 4; ++w) {
+                const double x = fin ? (double)v[u][4 * q + w] : 0.0;
                 const double y = ldexp(x, 6 - e);  // 64 x / s, exact
                 const double a0 = __builtin_rint(y);
                 const double y1 = (y - a0) * 128.0;  // exact
                 const double a1 = __builtin_rint(y1);
                 const double a2 = __builtin_rint((y1 - a1) * 128.0);
-                p0 |= ((int)a0 & 0xff) << (8 * u);
-                p1 |= ((int)a1 & 0xff) << (8 * u);
-                p2 |= ((int)a2 & 0xff) << (8 * u);
+                p0 |= ((int)a0 & 0xff) << (8 * w);
+                p1 |= ((int)a1 & 0xff) << (8 * w);
+                p2 |= ((int)a2 & 0xff) << (8 * w);
             }
             dig[0][q] = p0;
             dig[1][q] = p1;
@@ -210,7 +237,7 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                const int64_t *__restrict__ rb, int R, const int2 *__restrict__ order,
                const int *__restrict__ es, int n, int T64, double *__restrict__ part,
                int64_t ntile64) {
-    extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+    extern __shared__ __attribute__((aligned(16))) int8_t lds[];  // two stages of I8_STAGE bytes
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = blockIdx.x % R;
@@ -218,6 +245,7 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
     const int I = tile.x, J = tile.y;
     const int64_t k0 = rb[r], k1 = rb[r + 1];
     const int nch = (int)((k1 - k0) / I8_KC);
+#if BK_I8_PIPE == 1
     // staging: granule (operand o, digit t, row, g) of the chunk; thread t
     // moves 12: index q = tid + 256 u -> g = q & 3, row = (q >> 2) & 127,
     // t = (q >> 9) % 3, o = q / 1536
@@ -236,11 +264,11 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
 #pragma unroll
         for (int u = 0; u < 12; ++u) pf[u] = *reinterpret_cast<const v4i *>(src[u] + (int64_t)ch * I8_KC);
     };
-    auto put = [&](int stage) {
-        int8_t *b = lds + stage * I8_STAGE;
+    auto put = [&](int8_t *b) {
 #pragma unroll
         for (int u = 0; u < 12; ++u) *reinterpret_cast<v4i *>(b + dst[u]) = pf[u];
     };
+#endif
     v16i acc[3][2][2];
 #pragma unroll
     for (int l = 0; l < 3; ++l)
@@ -250,48 +278,149 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
             for (int b = 0; b < 2; ++b) acc[l][a][b] = v16i{};
     const int wr = (wave & 1) * 64, wc = (wave >> 1) * 64;
     const int fr = lane & 31, fh = lane >> 5;
+    // the fragments of k-step ks (32 columns: granules 2 ks + fh) of stage b
+    auto frags = [&](const int8_t *b, int ks, v4i (&fa)[3][2], v4i (&fb)[3][2]) {
+        const int g = 2 * ks + fh;
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const int ra = wr + 32 * a + fr, rbw = wc + 32 * a + fr;
+                fa[t][a] = *reinterpret_cast<const v4i *>(b + t * I8_PLANE + ra * I8_KC + 16 * i8_swz(ra, g));
+                fb[t][a] = *reinterpret_cast<const v4i *>(b + I8_OPND + t * I8_PLANE + rbw * I8_KC +
+                                                          16 * i8_swz(rbw, g));
+            }
+    };
+    auto mma = [&](const v4i (&fa)[3][2], const v4i (&fb)[3][2]) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+                acc[0][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[0][bb], acc[0][a][bb], 0, 0, 0);
+                acc[1][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[1][bb], acc[1][a][bb], 0, 0, 0);
+                acc[1][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][a], fb[0][bb], acc[1][a][bb], 0, 0, 0);
+                acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[2][bb], acc[2][a][bb], 0, 0, 0);
+                acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][a], fb[1][bb], acc[2][a][bb], 0, 0, 0);
+                acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][a], fb[0][bb], acc[2][a][bb], 0, 0, 0);
+            }
+    };
+    // Software pipeline at k-step granularity, one wave per SIMD: the MFMAs
+    // always run from registers while the same instruction stream moves the
+    // next operands, one memory instruction per MFMA gap (sched_group_barrier),
+    // so the matrix pipe does not wait on LDS.  Per chunk ch:
+    //   phase A: MFMAs of k-step 0 (F0)  | LDS reads of k-step 1 -> F1
+    //   barrier: every wave has read all of chunk ch and stored chunk ch + 1
+    //   phase B: MFMAs of k-step 1 (F1)  | LDS reads of chunk ch + 1's k-step 0
+    //            -> F0, chunk ch + 2 (fetched one chunk earlier) stored into
+    //            chunk ch's stage, chunk ch + 3 fetched
+    // Chunk indices past the range are clamped (a stage nobody reads again
+    // gets a stale copy; the last chunk is fetched again): no branch.
+#if BK_I8_PIPE == 1
     if (nch > 0) {
+        v4i F0a[3][2], F0b[3][2], F1a[3][2], F1b[3][2];
+        const auto cl = [&](int c) { return c < nch ? c : nch - 1; };
         fetch(0);
-        put(0);
-        if (nch > 1) fetch(1);
-    }
-    __syncthreads();
-    for (int ch = 0; ch < nch; ++ch) {
-        const int8_t *b = lds + (ch & 1) * I8_STAGE;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int g = 2 * ks + fh;
-            v4i fa[3][2], fb[3][2];
-#pragma unroll
-            for (int t = 0; t < 3; ++t)
-#pragma unroll
-                for (int a = 0; a < 2; ++a) {
-                    const int ra = wr + 32 * a + fr, rbw = wc + 32 * a + fr;
-                    fa[t][a] = *reinterpret_cast<const v4i *>(b + t * I8_PLANE + ra * I8_KC +
-                                                              16 * i8_swz(ra, g));
-                    fb[t][a] = *reinterpret_cast<const v4i *>(b + I8_OPND + t * I8_PLANE +
-                                                              rbw * I8_KC + 16 * i8_swz(rbw, g));
-                }
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int bb = 0; bb < 2; ++bb) {
-                    acc[0][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[0][bb], acc[0][a][bb], 0, 0, 0);
-                    acc[1][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[1][bb], acc[1][a][bb], 0, 0, 0);
-                    acc[1][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][a], fb[0][bb], acc[1][a][bb], 0, 0, 0);
-                    acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[2][bb], acc[2][a][bb], 0, 0, 0);
-                    acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][a], fb[1][bb], acc[2][a][bb], 0, 0, 0);
-                    acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][a], fb[0][bb], acc[2][a][bb], 0, 0, 0);
-                }
-        }
-        // the next chunk into the other stage (its previous readers finished
-        // at the barrier that ended chunk ch - 1), then prefetch ch + 2
-        if (ch + 1 < nch) {
-            put((ch + 1) & 1);
-            if (ch + 2 < nch) fetch(ch + 2);
-        }
+        put(lds);
+        fetch(cl(1));
+        put(lds + I8_STAGE);
+        fetch(cl(2));
         __syncthreads();
+        frags(lds, 0, F0a, F0b);
+        // chunk ch from stage C; chunk ch + 1 is in stage N, chunk ch + 2 goes
+        // to C.  __restrict__: the stages never overlap, so the compiler may
+        // interleave C's stores with N's reads (and both with the MFMAs)
+        auto body = [&](int ch, int8_t *__restrict__ C, const int8_t *__restrict__ N) {
+            mma(F0a, F0b);
+            frags(C, 1, F1a, F1b);
+#pragma unroll
+            for (int q = 0; q < 12; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // no motion across the phases
+            __syncthreads();
+            mma(F1a, F1b);
+            frags(N, 0, F0a, F0b);
+            put(C);
+            fetch(cl(ch + 3));
+#pragma unroll
+            for (int q = 0; q < 12; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        for (int ch = 0; ch < nch; ++ch)
+            body(ch, lds + (ch & 1) * I8_STAGE, lds + ((ch + 1) & 1) * I8_STAGE);
     }
+#else
+    // LDS-DMA: wave w moves 1-KiB pieces q = 12 w + u (u < 12) of each chunk:
+    // piece q is 16 rows of one (operand, digit) plane, lane l landing at
+    // q KiB + 16 l = row (l >> 2), slot l & 3, whose source granule is the
+    // slot un-swizzled.  Chunk c lives in stage c % 3 and is issued at chunk
+    // c - 2's phase A; a wave waits for its own pieces (vmcnt), the barrier
+    // for everyone's.
+    if (nch > 0) {
+        v4i F0a[3][2], F0b[3][2], F1a[3][2], F1b[3][2];
+        const auto cl = [&](int c) { return c < nch ? c : nch - 1; };
+        const int8_t *dsrc[12];
+#pragma unroll
+        for (int u = 0; u < 12; ++u) {
+            const int q = 12 * wave + u;
+            const int o = q / 24, t = (q >> 3) % 3, row = 16 * (q & 7) + (lane >> 2);
+            const int g = (lane & 3) ^ ((row >> 2) & 3);
+            const int grow = (o == 0 ? I : J) * I8_TILE + row;
+            dsrc[u] = S + (int64_t)t * plane + (int64_t)grow * dp + k0 + 16 * g;
+        }
+        auto dma = [&](int ch, int8_t *b) {
+#pragma unroll
+            for (int u = 0; u < 12; ++u)
+                __builtin_amdgcn_global_load_lds((const void *)(dsrc[u] + (int64_t)ch * I8_KC),
+                                                 (void *)(b + (12 * wave + u) * 1024), 16, 0, 0);
+        };
+        dma(0, lds);
+        dma(cl(1), lds + I8_STAGE);
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        __syncthreads();
+        frags(lds, 0, F0a, F0b);
+        // restrict: the three stages never overlap (C and N read, F written)
+        auto body = [&](int ch, const int8_t *__restrict__ C, const int8_t *__restrict__ N,
+                        int8_t *__restrict__ F) {
+            mma(F0a, F0b);
+            frags(C, 1, F1a, F1b);
+            dma(cl(ch + 2), F);
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (the LDS-DMA piece)
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // chunk ch + 1's pieces
+            __syncthreads();
+            mma(F1a, F1b);
+            frags(N, 0, F0a, F0b);
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        for (int ch = 0; ch < nch; ++ch) {
+            const int sc = ch % 3;
+            body(ch, lds + sc * I8_STAGE, lds + (sc == 2 ? 0 : sc + 1) * I8_STAGE,
+                 lds + (sc == 0 ? 2 : sc - 1) * I8_STAGE);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+    }
+#endif
     // epilogue: C/D lane l, reg e of a 32 x 32 block: row (e & 3) + 8 (e >> 2) + 4 (l >> 5), col l & 31
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -344,7 +473,6 @@ __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ pa
 // a row's slice of a range within 128 KiB, so k_i8_slice reads it once into
 // LDS (config E, fp32: 8 ranges of 32,768 columns; config D, fp64: 64 of
 // 16,384); <= 32,768 columns per range keeps every int32 sum exact
-constexpr int64_t I8_RANGE_BYTES = 131072;
 I8Layout i8_layout(int n, int64_t d, int es) {
     I8Layout L;
     L.npad = (n + I8_TILE - 1) / I8_TILE * I8_TILE;
@@ -385,15 +513,8 @@ size_t i8_workspace(const I8Layout &L) {
 }
 
 hipError_t configure_i8_kernels() {
-    hipError_t e = hipFuncSetAttribute((const void *)k_gram_i8,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, I8_LDS);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void *)k_i8_slice<float>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)I8_RANGE_BYTES);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void *)k_i8_slice<double>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)I8_RANGE_BYTES);
-    return e;
+    return hipFuncSetAttribute((const void *)k_gram_i8, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               I8_LDS);
 }
 
 static char *align256(char *p) { return (char *)(((uintptr_t)p + 255) & ~(uintptr_t)255); }
@@ -423,15 +544,15 @@ hipError_t launch_i8_slice(const void *X, int dtype, int64_t ld, int n, int64_t 
                            const I8Layout &L, void *ws, const void *tables, hipStream_t st) {
     const I8Ws w = i8_ws(L, ws);
     const int64_t *rb = (const int64_t *)tables;
-    int64_t lmax = 0;  // the longest range (LDS bytes of its row slice)
+    int64_t lmax = 0;  // the longest range: its row slice must fit the kernel's registers
     for (int r = 0; r < L.R; ++r) lmax = std::max<int64_t>(lmax, L.rb[r + 1] - L.rb[r]);
-    const size_t lds = (size_t)lmax * L.es;
+    if (lmax * L.es > I8_RANGE_BYTES) return hipErrorInvalidValue;
     if (dtype == 0)
-        hipLaunchKernelGGL(k_i8_slice<double>, dim3((unsigned)L.npad, (unsigned)L.R), dim3(256), lds,
-                           st, (const double *)X, ld, n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+        hipLaunchKernelGGL(k_i8_slice<double>, dim3((unsigned)L.npad, (unsigned)L.R), dim3(I8_SLICE_NT),
+                           0, st, (const double *)X, ld, n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
     else
-        hipLaunchKernelGGL(k_i8_slice<float>, dim3((unsigned)L.npad, (unsigned)L.R), dim3(256), lds,
-                           st, (const float *)X, ld, n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+        hipLaunchKernelGGL(k_i8_slice<float>, dim3((unsigned)L.npad, (unsigned)L.R), dim3(I8_SLICE_NT),
+                           0, st, (const float *)X, ld, n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_i8_bound, dim3(1), dim3(256), 0, st, w.es, w.l1, rb, L.R, n, d, w.bound);
