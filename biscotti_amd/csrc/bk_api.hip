@@ -639,8 +639,9 @@ int run_small(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_
         HIPCHK(hipMemsetAsync(c->trace.p, 0, twords * sizeof(long long), c->stream));
         trace = (long long *)c->trace.p;
     }
-    const uint64_t spin = c->small_spin_left == 0 ? SMALL_SPIN_MAX : c->small_spin_max;
-    if (c->small_spin_left > 0) --c->small_spin_left;
+    // (the test knob's count goes to launches that wait: a G-only launch has no hand-off)
+    const uint64_t spin = c->small_spin_left == 0 || !sm ? SMALL_SPIN_MAX : c->small_spin_max;
+    if (c->small_spin_left > 0 && sm) --c->small_spin_left;
     CHK(timed(c, BK_K_SMALL, [&] {
         return launch_small(dX, dtype, ld, (int)n, d, (int)f, sp, (double *)c->small_part.p,
                             (double *)c->U.p, sc, (double *)c->diag.p, d_sel, d_mean,
@@ -918,15 +919,17 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
             (void)hipGetLastError();  // not mapped (pinned by other means): copy it
         }
     }
-    // config B's verifier call (a host batch k_small takes, no noise): the copy
-    // in nc column chunks on the copy stream, each chunk's G items launched on
-    // the compute stream as soon as it has landed (an event, no spinning), so
-    // the Gram runs under the rest of the copy; then one S + M launch.  The
-    // same items and partials as the one-launch call: the same bits.
-    // BK_SMALL_PIPE=<chunks> (default 4; 0: one copy, then one launch)
+    // BK_SMALL_PIPE=<chunks> (A/B; default 0): the copy in that many column
+    // chunks on the copy stream, each chunk's G items launched on the compute
+    // stream as soon as it has landed (an event, no spinning), then one S + M
+    // launch -- the same items and partials as the one-launch call, the same
+    // bits.  Measured at config B (r4, tools/host_entry_ab.py): 0.157 ms per
+    // call with one copy, 0.201 with 2 chunks, 0.234 with 4 -- a strided
+    // column-chunk H2D and its launch cost more than the Gram they hide
+    // (~14 us), so the one copy + one launch stays the default
     static const int pipe_env = [] {
         const char *e = getenv("BK_SMALL_PIPE");
-        return e ? atoi(e) : 4;
+        return e ? atoi(e) : 0;
     }();
     const SmallPlan sp = small_plan((int)n, d, c->num_cu);
     int nc = 0;

@@ -204,18 +204,18 @@ def test_host_small_strided_view(engine, oracle, dtype, n, d, ld, f):
     assert np.max(np.abs(mean - omean)) <= 1e-9 * max(mscale, 1e-300)
 
 
-@pytest.mark.parametrize("n,d,f,dtype,pad", [
-    (100, 7850, 30, np.float64, 0),   # config B (mnist): 62 chunks, 4 pipelined copies
+HOST_SHAPES = [
+    (100, 7850, 30, np.float64, 0),   # config B (mnist): 62 chunks
     (100, 7849, 30, np.float64, 1),   # odd d, padded host rows
     (128, 2048, 60, np.float32, 0),   # the smallest pipelined batch (16 chunks)
     (37, 30001, 11, np.float64, 0),
-    (64, 4099, 20, np.float32, 3)])
-def test_host_entry_pipelined_bitwise(engine, oracle, n, d, f, dtype, pad):
-    """bk_multikrum from a host batch (pinned and pageable)
-    copies it in column chunks on the copy stream and launches each chunk's G
-    items as soon as it lands, then one S + M launch: the same items and
-    partials as the device-resident one-launch call, so the selection, scores
-    and mean are bitwise the device call's."""
+    (64, 4099, 20, np.float32, 3)]
+
+
+def _host_entry_check(engine, oracle, n, d, f, dtype, pad, launches):
+    """bk_multikrum from a host batch (pageable, then pinned) against the
+    device-resident one-launch call on the same rows: selection, scores and
+    mean bitwise; `launches` k_small launches and (one launch) one H2D."""
     import ctypes
     full = oracle.synth(n, d + pad, 4000 + n + d, f, dtype=dtype)
     Xv = full[:, :d]
@@ -224,7 +224,8 @@ def test_host_entry_pipelined_bitwise(engine, oracle, n, d, f, dtype, pad):
     got = engine.multikrum(Xv, f)  # pageable
     t = engine.timing_read()
     engine.timing_enable(False)
-    assert t["k_small"]["count"] == 5 and "h2d" not in t, t  # 4 G launches + 1 S+M launch
+    assert t["k_small"]["count"] == launches, t
+    assert ("h2d" in t) == (launches == 1), t
     for u, v in zip(got, ref):
         assert np.array_equal(u.view(np.uint8), v.view(np.uint8))
     # pinned (the verifier's stage_alloc buffers)
@@ -241,3 +242,43 @@ def test_host_entry_pipelined_bitwise(engine, oracle, n, d, f, dtype, pad):
     for u, v in zip((sel, sc, mean), ref):
         assert np.array_equal(u.view(np.uint8), v.view(np.uint8))
     engine.selection_margin()  # the S + M launch's record is readable (no hand-off error)
+
+
+@pytest.mark.parametrize("n,d,f,dtype,pad", HOST_SHAPES)
+def test_host_entry_bitwise(engine, oracle, n, d, f, dtype, pad):
+    """The default host entry for n <= 128: one H2D of the batch, one k_small
+    launch; bitwise the device call's outputs."""
+    _host_entry_check(engine, oracle, n, d, f, dtype, pad, launches=1)
+
+
+def test_host_entry_pipelined_bitwise():
+    """VERDICT r3 item 7, the A/B form (BK_SMALL_PIPE=4, read at bk_create,
+    so in a child process): the batch crosses PCIe in 4 column chunks on the
+    copy stream, each chunk's G items launch as soon as it lands, then one
+    S + M launch: the same items and partials as the one-launch call, so
+    every output is bitwise the device call's.  (Slower than one copy at
+    config B, 0.234 vs 0.157 ms per call: not the default)"""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    body = r"""
+import sys, os, json
+sys.path.insert(0, %r); sys.path.insert(0, os.path.join(%r, "tests"))
+sys.path.insert(0, os.path.join(%r, "tests", "golden"))
+import numpy as np, torch
+from biscotti_amd.krum import Engine
+from oracle import oracle as O
+import test_gpu_small as T
+eng = Engine(0)
+eng.set_stream(torch.cuda.current_stream().cuda_stream)
+for shp in T.HOST_SHAPES:
+    T._host_entry_check(eng, O, *shp, launches=5)
+print(json.dumps({"ok": True}))
+""" % (repo, repo, repo)
+    e = dict(os.environ, BK_SMALL_PIPE="4")
+    r = subprocess.run([sys.executable, "-c", body], env=e, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["ok"]
