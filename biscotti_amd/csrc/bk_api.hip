@@ -400,7 +400,7 @@ int get_i8(bk_ctx *c, int64_t n, int64_t d, int es, bk_ctx::I8Cached **out) {
     bk_ctx::I8Cached e;
     e.n = n;
     e.d = d;
-    e.L = i8_layout((int)n, d, es);
+    e.L = i8_layout((int)n, d, es, c->num_cu);
     const size_t tb = (size_t)(e.L.R + 1) * 8 + e.L.order.size() * sizeof(int);
     std::vector<char> h(tb);
     memcpy(h.data(), e.L.rb.data(), (size_t)(e.L.R + 1) * 8);

@@ -24,24 +24,26 @@
 // near_tie = 1.  A non-finite input makes that bound +inf (always a near tie;
 // BK_F32_I8_CERTIFIED re-runs it exact).
 //
-//   k_i8_slice   one workgroup per (row, range): the range's max |x| and
-//                ||x||_1 (one read), then the three digit planes (a second read,
-//                from L2): HBM-bound, 4 + 3 bytes per element
+//   k_i8_slice   one workgroup per (row, range): the range's row slice read
+//                once into registers, its max |x| and ||x||_1, then the three
+//                digit planes: HBM-bound, 4 (8) + 3 bytes per element
 //   k_i8_bound   the absolute error bound (one workgroup)
 //   k_gram_i8    128 x 128 output tiles of one range per workgroup, 4 waves of
 //                64 x 64 (2 x 2 MFMA blocks x 3 levels: 192 int32 accumulators
 //                per lane), digit planes staged through LDS in chunks of 64
 //                columns (48 KiB per stage, 2 stages), 16-B granules
 //                XOR-swizzled so every ds_read_b128 fragment read is
-//                conflict-free; workgroup b runs range b mod R (= its XCD when
-//                R = 8) and the (b / R)-th tile of a super-blocked order, so the
-//                32 CUs of an XCD share their row-blocks through its L2
+//                conflict-free; every XCD sweeps the column ranges in the same
+//                order over a compact piece of the tile order (i8_layout), so
+//                an XCD's concurrent tiles share row-blocks in its L2 and the
+//                XCDs share the range's digit lines in the Infinity Cache
 //   k_i8_reduce  U = sum over ranges (fixed order) of the exact range partials,
 //                + the trailing record {d, 0, bound, 0}
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "bk_internal.h"
@@ -64,6 +66,11 @@ constexpr int I8_STAGE = 2 * I8_OPND;              // 48 KiB
 #define BK_I8_PIPE 1
 #endif
 constexpr int I8_NSTAGE = BK_I8_PIPE == 3 ? 3 : 2;
+// K1i8's workgroup -> (tile, range) map (A/B builds): 0 = range b mod R, 1 =
+// every XCD on the same range at a time (i8_layout)
+#ifndef BK_I8_MAP
+#define BK_I8_MAP 1
+#endif
 constexpr int I8_LDS = I8_NSTAGE * I8_STAGE;       // 96 / 144 KiB
 constexpr int I8_RANGE_BYTES = 131072;             // a row's slice of one column range (i8_layout)
 
@@ -240,9 +247,11 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
     extern __shared__ __attribute__((aligned(16))) int8_t lds[];  // two stages of I8_STAGE bytes
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = blockIdx.x % R;
-    const int2 tile = order[blockIdx.x / R];
-    const int I = tile.x, J = tile.y;
+    // this workgroup's item: its 128-row tile (I | J << 16) and column range
+    // (i8_layout; r < 0: a padding workgroup of a short XCD list)
+    const int2 item = order[blockIdx.x];
+    if (item.y < 0) return;
+    const int r = item.y, I = item.x & 0xffff, J = item.x >> 16;
     const int64_t k0 = rb[r], k1 = rb[r + 1];
     const int nch = (int)((k1 - k0) / I8_KC);
 #if BK_I8_PIPE == 1
@@ -291,18 +300,20 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                                                           16 * i8_swz(rbw, g));
             }
     };
+    // the six digit products of one k-step, product-major over the 2 x 2
+    // blocks: consecutive MFMAs never accumulate into the same registers (a
+    // block's L1 and L2 chains are 4 MFMAs apart), so none waits on the one
+    // before it (r4b ran each chain back to back: MFMA busy 62 %)
     auto mma = [&](const v4i (&fa)[3][2], const v4i (&fb)[3][2]) {
+        constexpr int PT[6][3] = {{0, 0, 0}, {1, 0, 1}, {1, 1, 0}, {2, 0, 2}, {2, 1, 1}, {2, 2, 0}};
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int p = 0; p < 6; ++p)
 #pragma unroll
-            for (int bb = 0; bb < 2; ++bb) {
-                acc[0][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[0][bb], acc[0][a][bb], 0, 0, 0);
-                acc[1][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[1][bb], acc[1][a][bb], 0, 0, 0);
-                acc[1][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][a], fb[0][bb], acc[1][a][bb], 0, 0, 0);
-                acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][a], fb[2][bb], acc[2][a][bb], 0, 0, 0);
-                acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][a], fb[1][bb], acc[2][a][bb], 0, 0, 0);
-                acc[2][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][a], fb[0][bb], acc[2][a][bb], 0, 0, 0);
-            }
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb)
+                    acc[PT[p][0]][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                        fa[PT[p][1]][a], fb[PT[p][2]][bb], acc[PT[p][0]][a][bb], 0, 0, 0);
     };
     // Software pipeline at k-step granularity, one wave per SIMD: the MFMAs
     // always run from registers while the same instruction stream moves the
@@ -470,10 +481,14 @@ __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ pa
 // host side
 // ---------------------------------------------------------------------------
 // R column ranges: at least one per XCD, and as many more (in eights) as keep
-// a row's slice of a range within 128 KiB, so k_i8_slice reads it once into
-// LDS (config E, fp32: 8 ranges of 32,768 columns; config D, fp64: 64 of
-// 16,384); <= 32,768 columns per range keeps every int32 sum exact
-I8Layout i8_layout(int n, int64_t d, int es) {
+// a row's slice of a range within 128 KiB, so k_i8_slice holds it in
+// registers (config E, fp32: 8 ranges of 32,768 columns; config D, fp64: 64 of
+// 16,384); <= 32,768 columns per range keeps every int32 sum exact.  Then, if
+// the (tile, range) items leave the last round of workgroups on an XCD well
+// short of full, R is raised (in eights, up to 4x, ranges >= 16 chunks) to the
+// count that fills the rounds (config D: 10 tiles x 64 ranges = 2.5 rounds of
+// 32 CUs per XCD -> 128 ranges, 5 rounds; config E stays at 8: 16.5 of 17)
+I8Layout i8_layout(int n, int64_t d, int es, int num_cu) {
     I8Layout L;
     L.npad = (n + I8_TILE - 1) / I8_TILE * I8_TILE;
     L.dp = (d + I8_KC - 1) / I8_KC * I8_KC;
@@ -481,7 +496,21 @@ I8Layout i8_layout(int n, int64_t d, int es) {
     const int64_t cmax = I8_RANGE_BYTES / es;  // columns per range
     int64_t R = (L.dp + cmax - 1) / cmax;
     R = (R + 7) / 8 * 8;
-    L.R = (int)(nk < R ? nk : R);
+    R = nk < R ? nk : R;
+    {
+        const int T = L.npad / I8_TILE;
+        const int64_t NT = (int64_t)T * (T + 1) / 2;
+        const double cx = num_cu > 0 ? num_cu / 8.0 : 32.0;  // CUs per XCD
+        auto eff = [&](int64_t r) {
+            const double rounds = (double)((NT * r + 7) / 8) / cx;
+            return rounds / std::ceil(rounds);
+        };
+        int64_t best = R;
+        for (int64_t r = R + 8; r <= 4 * R && nk / r >= 16; r += 8)
+            if (eff(r) > eff(best) + 0.05) best = r;
+        R = best;
+    }
+    L.R = (int)R;
     L.es = es;
     L.rb.resize(L.R + 1);
     for (int r = 0; r <= L.R; ++r) L.rb[r] = nk * r / L.R * I8_KC;
@@ -490,18 +519,51 @@ I8Layout i8_layout(int n, int64_t d, int es) {
     L.T64 = (n + 63) / 64;
     L.ntile64 = (int64_t)L.T64 * (L.T64 + 1) / 2;
     // super-blocked upper-triangle order of the 128-row tiles: blocks of 4 x 4
-    // tiles row by row, so the CUs of an XCD, which take consecutive tiles,
-    // share their row-blocks through its L2
+    // tiles row by row, so consecutive tiles share row-blocks
     constexpr int SB = 4;
     const int T = L.T128, NB = (T + SB - 1) / SB;
+    std::vector<int> tiles;  // I | J << 16
     for (int BI = 0; BI < NB; ++BI)
         for (int BJ = BI; BJ < NB; ++BJ)
             for (int I = BI * SB; I < BI * SB + SB && I < T; ++I)
                 for (int J = BJ * SB; J < BJ * SB + SB && J < T; ++J)
-                    if (I <= J) {
-                        L.order.push_back(I);
-                        L.order.push_back(J);
-                    }
+                    if (I <= J) tiles.push_back(I | J << 16);
+    const int NT = (int)tiles.size();
+#if BK_I8_MAP == 0
+    // r3/r4a: workgroup b runs range b mod R (= its XCD when R = 8) and tile b / R
+    for (int b = 0; b < NT * L.R; ++b) {
+        L.order.push_back(tiles[b / L.R]);
+        L.order.push_back(b % L.R);
+    }
+#else
+    // Workgroup b runs on XCD b mod 8 (dispatch order; speed only).  Every XCD
+    // sweeps the ranges in the same order, taking a contiguous piece of the
+    // tile order per range (ceil or floor of NT / 8 tiles, the extra tiles
+    // rotating over the XCDs so the totals balance): at any time the whole
+    // chip works on one column range, so the digit lines one XCD fetches are
+    // found in the Infinity Cache by the others, while each XCD's concurrent
+    // tiles stay compact (few row-blocks per chunk in its L2)
+    std::vector<std::vector<int>> per(8);
+    for (int r = 0; r < L.R; ++r) {
+        const int q = NT / 8, rem = NT % 8;
+        int j = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int cnt = q + (((x - r) % 8 + 8) % 8 < rem ? 1 : 0);
+            for (int k = 0; k < cnt; ++k, ++j) {
+                per[x].push_back(tiles[j]);
+                per[x].push_back(r);
+            }
+        }
+    }
+    size_t mx = 0;
+    for (auto &v : per) mx = std::max(mx, v.size() / 2);
+    for (size_t sidx = 0; sidx < mx; ++sidx)
+        for (int x = 0; x < 8; ++x) {
+            const bool on = sidx < per[x].size() / 2;
+            L.order.push_back(on ? per[x][2 * sidx] : 0);
+            L.order.push_back(on ? per[x][2 * sidx + 1] : -1);
+        }
+#endif
     return L;
 }
 
@@ -563,8 +625,8 @@ hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables
     const I8Ws w = i8_ws(L, ws);
     const int64_t *rb = (const int64_t *)tables;  // {rb (R + 1 int64), order (int pairs)}
     const int2 *order = (const int2 *)((const char *)tables + (size_t)(L.R + 1) * 8);
-    const int64_t ntiles = (int64_t)L.order.size() / 2;
-    hipLaunchKernelGGL(k_gram_i8, dim3((unsigned)(ntiles * L.R)), dim3(256), I8_LDS, st, w.S, L.dp,
+    const int64_t items = (int64_t)L.order.size() / 2;  // one workgroup each
+    hipLaunchKernelGGL(k_gram_i8, dim3((unsigned)items), dim3(256), I8_LDS, st, w.S, L.dp,
                        L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
     return hipGetLastError();
 }

@@ -180,9 +180,9 @@ struct I8Layout {
     int npad = 0, R = 0, T128 = 0, T64 = 0, es = 4;
     int64_t dp = 0, plane = 0, ntile64 = 0;
     std::vector<int64_t> rb;  // range boundaries (R + 1, multiples of 64 columns)
-    std::vector<int> order;   // the 128-row tiles (I <= J), super-blocked: pairs
+    std::vector<int> order;   // per workgroup {tile I | J << 16, range (-1: idle)}
 };
-I8Layout i8_layout(int n, int64_t d, int es);
+I8Layout i8_layout(int n, int64_t d, int es, int num_cu);
 size_t i8_workspace(const I8Layout &L);
 hipError_t configure_i8_kernels();
 // tables: device copy of {rb (R + 1 int64), order (int pairs)}; ws:

@@ -17,6 +17,8 @@ item 4).  The reference's Gram is np.dot(X, X.T) in fp64
   term.
 * Non-finite input: the bound is +inf (always a near tie).
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -40,15 +42,30 @@ def _upper(engine, X, mode):
     return U.cpu().numpy()
 
 
-def _ranges(d, es):
+def _ranges(n, d, es, num_cu=256):
     """bk_i8.hip i8_layout: R column ranges of whole 64-column granules, at
-    least 8, in eights, each row slice <= 128 KiB."""
+    least 8, in eights, each row slice <= 128 KiB; then raised (in eights, up
+    to 4x, ranges >= 16 chunks) when that fills the XCDs' last round of
+    (tile, range) workgroups by more than 5 points."""
     dp = (d + 63) // 64 * 64
     nk = dp // 64
     cmax = 131072 // es
     R = -(-dp // cmax)
     R = -(-R // 8) * 8
     R = min(nk, R)
+    T = -(-n // 128)
+    NT = T * (T + 1) // 2
+    cx = num_cu / 8.0
+
+    def eff(r):
+        rounds = (-(-(NT * r) // 8)) / cx
+        return rounds / math.ceil(rounds)
+    best, r = R, R + 8
+    while r <= 4 * R and nk // r >= 16:
+        if eff(r) > eff(best) + 0.05:
+            best = r
+        r += 8
+    R = best
     return [(nk * r // R * 64, nk * (r + 1) // R * 64) for r in range(R)]
 
 
@@ -57,7 +74,7 @@ def _bound(X):
     es = X.dtype.itemsize
     X = X.astype(np.float64)
     tot = 0.0
-    for c0, c1 in _ranges(X.shape[1], es):
+    for c0, c1 in _ranges(X.shape[0], X.shape[1], es):
         A = np.abs(X[:, c0:min(c1, X.shape[1])])
         if A.shape[1] == 0:
             continue
