@@ -836,7 +836,14 @@ def main():
 
     eng = Engine(dev_idx)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    eng.set_f32_mode(F32_MODES[a.f32_mode])
+    # fp64 rows take the int8 modes through bk_set_f64_mode (K1i8 for fp64 rows)
+    f64_i8 = w["dtype"] == "f64" and a.f32_mode in ("i8", "i8_certified")
+    if w["dtype"] == "f64" and a.f32_mode not in ("exact", "i8", "i8_certified"):
+        raise SystemExit("--f32-mode %s applies to fp32 rows only" % a.f32_mode)
+    if f64_i8:
+        eng.set_f64_mode(F32_MODES[a.f32_mode])
+    else:
+        eng.set_f32_mode(F32_MODES[a.f32_mode])
     if sharded and not host_exch:
         if tdist.is_initialized():
             bootstrap_rccl(eng, rank, world, torch_broadcast_bytes)
@@ -1009,7 +1016,7 @@ def main():
                                                          "RCCL all-reduce"))
                    if sharded and not emu else
                    ("emulated rank 0 of %d (1 GPU)" % emu if emu else "1 GPU"),
-                   "d_local": dl, **({"f32_mode": a.f32_mode} if w["dtype"] == "f32" else {})},
+                   "d_local": dl, **({"f32_mode": a.f32_mode} if w["dtype"] == "f32" or f64_i8 else {})},
         "roofline": roof,
         "roofline_hbm_k4": k4_roof,
         "step_roofline": step_roof,
@@ -1103,7 +1110,10 @@ def main():
                 V[nm]["host_entry"] = host_entry_variant(eng, dev, nm)
                 if cpu:
                     V[nm]["cpu_baseline"] = cpu_baseline(WORKLOADS[nm], 3.0, 2.0)
-        eng.set_f32_mode(F32_MODES[a.f32_mode])  # the line's own mode for what follows
+        if f64_i8:  # the line's own mode for what follows
+            eng.set_f64_mode(F32_MODES[a.f32_mode])
+        else:
+            eng.set_f32_mode(F32_MODES[a.f32_mode])
 
     if rank == 0 and world == 1 and not emu and a.workload == DEFAULT_WORKLOAD and not a.no_graph_probe:
         out["hip_graph"] = graph_probe(eng, dev, X, n, d, f, sel, scores, mean, bdt)
