@@ -66,6 +66,23 @@ constexpr int I8_STAGE = 2 * I8_OPND;              // 48 KiB
 #define BK_I8_PIPE 1
 #endif
 constexpr int I8_NSTAGE = BK_I8_PIPE == 3 ? 3 : 2;
+// digit-plane layout (A/B builds): 0 = row-major (row i's range at i * dp),
+// 1 = blocked per (row-block of 128, 64-column chunk): 8 KiB contiguous, so a
+// chunk fetch of a row-block is one 8-KiB run instead of 128 64-B pieces
+#ifndef BK_I8_BLOCKED
+#define BK_I8_BLOCKED 1
+#endif
+// byte offset of (row, column) in one digit plane (column a multiple of 16
+// for the 16-B stores and loads; dp = padded columns)
+__host__ __device__ __forceinline__ int64_t i8_off(int64_t row, int64_t col, int64_t dp) {
+#if BK_I8_BLOCKED
+    return (((row >> 7) * (dp >> 6) + (col >> 6)) << 13) + ((row & 127) << 6) + (col & 63);
+#else
+    return row * dp + col;
+#endif
+}
+// bytes between consecutive 64-column chunks of one row
+constexpr int64_t I8_CHUNK_STRIDE = BK_I8_BLOCKED ? 8192 : I8_KC;
 // K1i8's workgroup -> (tile, range) map (A/B builds): 0 = range b mod R, 1 =
 // every XCD on the same range at a time (i8_layout)
 #ifndef BK_I8_MAP
@@ -99,7 +116,16 @@ __global__ __launch_bounds__(I8_SLICE_NT) void k_i8_slice(const T *__restrict__ 
     typedef T gvec __attribute__((ext_vector_type(EPG)));
     __shared__ double smx[I8_SLICE_NT / 64], sl1[I8_SLICE_NT / 64];
     __shared__ int sfin[I8_SLICE_NT / 64];
-    const int i = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+#if BK_I8_BLOCKED
+    // rows 2k and 2k + 1 (the two 64-B halves of every 128-B line the blocked
+    // layout writes) on the same XCD, 8 blocks apart in dispatch order, so its
+    // L2 merges the halves before they go to memory
+    const int bx = blockIdx.x;
+    const int i = (bx & ~15) | ((bx & 7) << 1) | ((bx >> 3) & 1);
+#else
+    const int i = blockIdx.x;
+#endif
+    const int r = blockIdx.y, tid = threadIdx.x;
     const int64_t c0 = rb[r], c1 = rb[r + 1];
     const int64_t ce = c1 < d ? c1 : d;  // columns past d are zero
     const int len = (int)(c1 - c0);      // a multiple of 64, <= MAXU * BLK
@@ -160,7 +186,7 @@ __global__ __launch_bounds__(I8_SLICE_NT) void k_i8_slice(const T *__restrict__ 
         es[(int64_t)i * R + r] = e;
         l1o[(int64_t)i * R + r] = fin ? l1 : __builtin_inf();
     }
-    int8_t *s0 = S + (int64_t)i * dp + c0, *s1 = s0 + plane, *s2 = s1 + plane;
+    int8_t *s0 = S, *s1 = s0 + plane, *s2 = s1 + plane;
 #pragma unroll
     for (int u = 0; u < MAXU; ++u) {
         const int c = u * BLK + 16 * tid;
@@ -185,9 +211,10 @@ __global__ __launch_bounds__(I8_SLICE_NT) void k_i8_slice(const T *__restrict__ 
             dig[1][q] = p1;
             dig[2][q] = p2;
         }
-        *reinterpret_cast<v4i *>(s0 + c) = v4i{dig[0][0], dig[0][1], dig[0][2], dig[0][3]};
-        *reinterpret_cast<v4i *>(s1 + c) = v4i{dig[1][0], dig[1][1], dig[1][2], dig[1][3]};
-        *reinterpret_cast<v4i *>(s2 + c) = v4i{dig[2][0], dig[2][1], dig[2][2], dig[2][3]};
+        const int64_t o = i8_off(i, c0 + c, dp);
+        *reinterpret_cast<v4i *>(s0 + o) = v4i{dig[0][0], dig[0][1], dig[0][2], dig[0][3]};
+        *reinterpret_cast<v4i *>(s1 + o) = v4i{dig[1][0], dig[1][1], dig[1][2], dig[1][3]};
+        *reinterpret_cast<v4i *>(s2 + o) = v4i{dig[2][0], dig[2][1], dig[2][2], dig[2][3]};
     }
 }
 
@@ -265,13 +292,13 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
         const int q = tid + 256 * u;
         const int g = q & 3, row = (q >> 2) & 127, t = (q >> 9) % 3, o = q / 1536;
         const int grow = (o == 0 ? I : J) * I8_TILE + row;
-        src[u] = S + (int64_t)t * plane + (int64_t)grow * dp + k0 + 16 * g;
+        src[u] = S + (int64_t)t * plane + i8_off(grow, k0 + 16 * g, dp);
         dst[u] = o * I8_OPND + t * I8_PLANE + row * I8_KC + 16 * i8_swz(row, g);
     }
     v4i pf[12];
     auto fetch = [&](int ch) {
 #pragma unroll
-        for (int u = 0; u < 12; ++u) pf[u] = *reinterpret_cast<const v4i *>(src[u] + (int64_t)ch * I8_KC);
+        for (int u = 0; u < 12; ++u) pf[u] = *reinterpret_cast<const v4i *>(src[u] + (int64_t)ch * I8_CHUNK_STRIDE);
     };
     auto put = [&](int8_t *b) {
 #pragma unroll
@@ -386,12 +413,12 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
             const int o = q / 24, t = (q >> 3) % 3, row = 16 * (q & 7) + (lane >> 2);
             const int g = (lane & 3) ^ ((row >> 2) & 3);
             const int grow = (o == 0 ? I : J) * I8_TILE + row;
-            dsrc[u] = S + (int64_t)t * plane + (int64_t)grow * dp + k0 + 16 * g;
+            dsrc[u] = S + (int64_t)t * plane + i8_off(grow, k0 + 16 * g, dp);
         }
         auto dma = [&](int ch, int8_t *b) {
 #pragma unroll
             for (int u = 0; u < 12; ++u)
-                __builtin_amdgcn_global_load_lds((const void *)(dsrc[u] + (int64_t)ch * I8_KC),
+                __builtin_amdgcn_global_load_lds((const void *)(dsrc[u] + (int64_t)ch * I8_CHUNK_STRIDE),
                                                  (void *)(b + (12 * wave + u) * 1024), 16, 0, 0);
         };
         dma(0, lds);
