@@ -795,6 +795,12 @@ def main():
                     help="tuning aid on a 1-GPU box: run rank 0's column shard of an N-rank "
                          "job (sharded path, 1-rank RCCL exchange); value is that rank's rate")
     a = ap.parse_args()
+    # the JSON line is the only thing on stdout: libraries that print banners
+    # to fd 1 (RCCL's init prints its version block there) are sent to stderr,
+    # and the line goes to the saved stdout at the end
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1164,7 +1170,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
 
     if rank == 0:
-        print(json.dumps(compact_line(out, a.detail_out)), flush=True)
+        os.write(json_fd, (json.dumps(compact_line(out, a.detail_out)) + "\n").encode())
     if tdist.is_initialized():
         tdist.barrier()
         tdist.destroy_process_group()

@@ -102,20 +102,23 @@ constexpr int I8_RANGE_BYTES = 131072;             // a row's slice of one colum
 // T = float (config E) or double (fp64 rows: the same digits, every step
 // exact in fp64 too; only the remainder past the third digit is dropped)
 // ---------------------------------------------------------------------------
+// NT threads, MAXU blocks of 16 NT columns: <512, full> for the ranges of a
+// whole batch; <256, 1> for ranges of <= 4,096 columns (a column shard's
+// ranges: config E's 8-rank shard has 4,096 per range), where 512 threads
+// would leave half idle and every register block but one unused
 constexpr int I8_SLICE_NT = 512;
-template <typename T>
-__global__ __launch_bounds__(I8_SLICE_NT) void k_i8_slice(const T *__restrict__ X, int64_t ld, int n,
-                                                          int64_t d, const int64_t *__restrict__ rb,
-                                                          int R, int8_t *__restrict__ S, int64_t dp,
-                                                          int64_t plane, int *__restrict__ es,
-                                                          double *__restrict__ l1o) {
-    constexpr int EPG = 16 / sizeof(T);                               // elements per 16-B load
-    constexpr int BLK = 16 * I8_SLICE_NT;                             // columns per block
-    constexpr int MAXU = I8_RANGE_BYTES / (int)(sizeof(T) * BLK);     // blocks per range
-    static_assert(MAXU >= 1 && MAXU * BLK * (int)sizeof(T) == I8_RANGE_BYTES, "range blocks");
+template <typename T, int NT = I8_SLICE_NT,
+          int MAXU = I8_RANGE_BYTES / (int)(sizeof(T) * 16 * I8_SLICE_NT)>
+__global__ __launch_bounds__(NT) void k_i8_slice(const T *__restrict__ X, int64_t ld, int n,
+                                                 int64_t d, const int64_t *__restrict__ rb, int R,
+                                                 int8_t *__restrict__ S, int64_t dp, int64_t plane,
+                                                 int *__restrict__ es, double *__restrict__ l1o) {
+    constexpr int EPG = 16 / sizeof(T);  // elements per 16-B load
+    constexpr int BLK = 16 * NT;         // columns per block
+    static_assert(MAXU >= 1 && MAXU * BLK * (int)sizeof(T) <= I8_RANGE_BYTES, "range blocks");
     typedef T gvec __attribute__((ext_vector_type(EPG)));
-    __shared__ double smx[I8_SLICE_NT / 64], sl1[I8_SLICE_NT / 64];
-    __shared__ int sfin[I8_SLICE_NT / 64];
+    __shared__ double smx[NT / 64], sl1[NT / 64];
+    __shared__ int sfin[NT / 64];
 #if BK_I8_BLOCKED
     // rows 2k and 2k + 1 (the two 64-B halves of every 128-B line the blocked
     // layout writes) on the same XCD, 8 blocks apart in dispatch order, so its
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(I8_SLICE_NT) void k_i8_slice(const T *__restrict__ 
     l1 = sl1[0];
     fin = sfin[0];
 #pragma unroll
-    for (int w = 1; w < I8_SLICE_NT / 64; ++w) {
+    for (int w = 1; w < NT / 64; ++w) {
         mx = smx[w] > mx ? smx[w] : mx;
         l1 += sl1[w];
         fin &= sfin[w];
@@ -637,12 +640,20 @@ hipError_t launch_i8_slice(const void *X, int dtype, int64_t ld, int n, int64_t 
     int64_t lmax = 0;  // the longest range: its row slice must fit the kernel's registers
     for (int r = 0; r < L.R; ++r) lmax = std::max<int64_t>(lmax, L.rb[r + 1] - L.rb[r]);
     if (lmax * L.es > I8_RANGE_BYTES) return hipErrorInvalidValue;
-    if (dtype == 0)
-        hipLaunchKernelGGL(k_i8_slice<double>, dim3((unsigned)L.npad, (unsigned)L.R), dim3(I8_SLICE_NT),
-                           0, st, (const double *)X, ld, n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+    const dim3 grid((unsigned)L.npad, (unsigned)L.R);
+    const bool shortr = lmax <= 16 * 256;  // every range fits <256, 1>
+    if (dtype == 0 && shortr)
+        hipLaunchKernelGGL((k_i8_slice<double, 256, 1>), grid, dim3(256), 0, st, (const double *)X, ld,
+                           n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+    else if (dtype == 0)
+        hipLaunchKernelGGL(k_i8_slice<double>, grid, dim3(I8_SLICE_NT), 0, st, (const double *)X, ld, n,
+                           d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+    else if (shortr)
+        hipLaunchKernelGGL((k_i8_slice<float, 256, 1>), grid, dim3(256), 0, st, (const float *)X, ld, n,
+                           d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
     else
-        hipLaunchKernelGGL(k_i8_slice<float>, dim3((unsigned)L.npad, (unsigned)L.R), dim3(I8_SLICE_NT),
-                           0, st, (const float *)X, ld, n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+        hipLaunchKernelGGL(k_i8_slice<float>, grid, dim3(I8_SLICE_NT), 0, st, (const float *)X, ld, n, d,
+                           rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_i8_bound, dim3(1), dim3(256), 0, st, w.es, w.l1, rb, L.R, n, d, w.bound);

@@ -40,8 +40,10 @@ def test_bench_two_ranks_host_exchange(workload):
            "--no-graph-probe", "--no-variants"]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-4000:]
-    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints ONE line
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    # rank 0 prints ONE line and nothing else reaches stdout (library banners
+    # such as RCCL's version block go to stderr)
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 3
     assert out["config"]["d_local"] < out["config"]["d"]  # rank 0 holds a column shard
