@@ -62,7 +62,7 @@ def main():
     lib0.bk_synth_fill_device(ctx0, X.data_ptr(), dt, n, d, d, 0, d, 1, n // 3, 0.01, 0.05, 1e-3, 0)
     lib0.bk_synchronize(ctx0)
     for label, lib, ctx, env in builds:
-        st = (lib.bk_set_f64_mode(ctx, 1) if f64 else lib.bk_set_f32_mode(ctx, 3))
+        st = (lib.bk_set_f64_mode(ctx, 3) if f64 else lib.bk_set_f32_mode(ctx, 3))
         assert st == 0, lib.bk_last_error()
     ue = int(lib0.bk_upper_elems(n))
     Us = {b[0]: torch.empty(ue, dtype=torch.float64, device="cuda") for b in builds}
