@@ -27,7 +27,7 @@
 //   k_i8_slice   one workgroup per (row, range): the range's row slice read
 //                once into registers, its max |x| and ||x||_1, then the three
 //                digit planes: HBM-bound, 4 (8) + 3 bytes per element
-//   k_i8_bound   the absolute error bound (one workgroup)
+//   k_i8_bound   the absolute error bound (one workgroup, a wave per range)
 //   k_gram_i8    128 x 128 output tiles of one range per workgroup, 4 waves of
 //                64 x 64 (2 x 2 MFMA blocks x 3 levels: 192 int32 accumulators
 //                per lane), digit planes staged through LDS in chunks of 64
@@ -222,42 +222,44 @@ __global__ __launch_bounds__(NT) void k_i8_slice(const T *__restrict__ X, int64_
 }
 
 // the absolute error bound of the sliced Gram (header), into out[0]
-__global__ __launch_bounds__(256) void k_i8_bound(const int *__restrict__ es,
-                                                  const double *__restrict__ l1,
-                                                  const int64_t *__restrict__ rb, int R, int n,
-                                                  int64_t d, double *__restrict__ out) {
-    __shared__ double ssm[4], slm[4];
+// one workgroup of 16 waves: wave w takes ranges w, w + 16, ... (its lanes
+// over the rows: the max scale and the max norm of the range, exact whatever
+// the order; a NaN / inf norm is sticky), the range's term goes to LDS, and
+// thread 0 adds the terms in range order -- the same sum as one thread looping
+// over the ranges (r4c's form: 71 us at config D's 128 ranges, on the path)
+constexpr int I8_BOUND_NT = 1024, I8_BOUND_BATCH = 1024;
+__global__ __launch_bounds__(I8_BOUND_NT) void k_i8_bound(const int *__restrict__ es,
+                                                          const double *__restrict__ l1,
+                                                          const int64_t *__restrict__ rb, int R, int n,
+                                                          int64_t d, double *__restrict__ out) {
+    __shared__ double term[I8_BOUND_BATCH];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double tot = 0.0;
-    for (int r = 0; r < R; ++r) {
-        double smax = 0.0, lmax = 0.0;
-        for (int i = threadIdx.x; i < n; i += 256) {
-            const double s = ldexp(1.0, es[(int64_t)i * R + r]);
-            const double v = l1[(int64_t)i * R + r];
-            smax = s > smax ? s : smax;
-            lmax = (v > lmax || v != v) ? v : lmax;  // a NaN / inf norm poisons the bound
-        }
+    for (int r0 = 0; r0 < R; r0 += I8_BOUND_BATCH) {
+        const int r1 = R - r0 < I8_BOUND_BATCH ? R : r0 + I8_BOUND_BATCH;
+        for (int r = r0 + wave; r < r1; r += I8_BOUND_NT / 64) {
+            double smax = 0.0, lmax = 0.0;
+            for (int i = lane; i < n; i += 64) {
+                const double sv = ldexp(1.0, es[(int64_t)i * R + r]);
+                const double v = l1[(int64_t)i * R + r];
+                smax = sv > smax ? sv : smax;
+                lmax = (v > lmax || v != v) ? v : lmax;  // a NaN / inf norm poisons the bound
+            }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const double a = __shfl_xor(smax, o), b = __shfl_xor(lmax, o);
-            smax = a > smax ? a : smax;
-            lmax = (b > lmax || b != b) ? b : lmax;
-        }
-        if ((threadIdx.x & 63) == 0) {
-            ssm[threadIdx.x >> 6] = smax;
-            slm[threadIdx.x >> 6] = lmax;
+            for (int o = 32; o > 0; o >>= 1) {
+                const double x = __shfl_xor(smax, o), y = __shfl_xor(lmax, o);
+                smax = x > smax ? x : smax;
+                lmax = (y > lmax || y != y) ? y : lmax;
+            }
+            if (lane == 0) {
+                const int64_t c1 = rb[r + 1] < d ? rb[r + 1] : d;
+                const double dr = (double)(c1 > rb[r] ? c1 - rb[r] : 0);
+                term[r - r0] = 0x1p-21 * (2.0 * smax * lmax + 2.03 * dr * smax * smax);
+            }
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int w = 1; w < 4; ++w) {
-                smax = ssm[w] > smax ? ssm[w] : smax;
-                lmax = (slm[w] > lmax || slm[w] != slm[w]) ? slm[w] : lmax;
-            }
-            smax = ssm[0] > smax ? ssm[0] : smax;
-            lmax = (slm[0] > lmax || slm[0] != slm[0]) ? slm[0] : lmax;
-            const int64_t c1 = rb[r + 1] < d ? rb[r + 1] : d;
-            const double dr = (double)(c1 > rb[r] ? c1 - rb[r] : 0);
-            tot += 0x1p-21 * (2.0 * smax * lmax + 2.03 * dr * smax * smax);
-        }
+        if (threadIdx.x == 0)
+            for (int r = r0; r < r1; ++r) tot += term[r - r0];
         __syncthreads();
     }
     if (threadIdx.x == 0) out[0] = (tot == tot && tot < __builtin_inf()) ? tot * (1.0 + 0x1p-20)
@@ -656,7 +658,7 @@ hipError_t launch_i8_slice(const void *X, int dtype, int64_t ld, int n, int64_t 
                            rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_i8_bound, dim3(1), dim3(256), 0, st, w.es, w.l1, rb, L.R, n, d, w.bound);
+    hipLaunchKernelGGL(k_i8_bound, dim3(1), dim3(I8_BOUND_NT), 0, st, w.es, w.l1, rb, L.R, n, d, w.bound);
     return hipGetLastError();
 }
 
