@@ -142,8 +142,8 @@ enum bk_f32_mode {
     BK_F32_I8_CERTIFIED = 4
 };
 /* BK_F32_I8: the Gram from exact int8 digit slices on v_mfma_i32_32x32x32_i8
- * (bk_i8.hip, K1i8; the Ozaki scheme).  Per range of columns (one per XCD)
- * every row is scaled by a power of two >= its max |x| and cut into three
+ * (bk_i8.hip, K1i8; the Ozaki scheme).  Per range of columns (at least 8,
+ * each row's slice <= 128 KiB) every row is scaled by a power of two >= its max |x| and cut into three
  * signed 7-bit digits; the six digit products of weight >= 2^-26 accumulate
  * exactly in int32 and combine exactly in fp64, so each range's partial is
  * exact for the truncated digits and the result deterministic.  The dropped
