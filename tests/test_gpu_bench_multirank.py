@@ -52,3 +52,20 @@ def test_bench_two_ranks_host_exchange(workload):
     assert not out["parity"]["margin"]["near_tie"]
     assert out["rccl"]["nranks"] == 2 and out["rccl"]["ranks_agree"], out["rccl"]
     assert out["value"] > 0 and out["ms_per_step"] > 0
+
+
+def test_bench_stdout_is_one_json_line_with_rccl():
+    """The driver parses bench.py's stdout: with RCCL initialised (the sharded
+    path at one rank, as every rank of the 8-GPU run initialises it) RCCL
+    prints its version block to fd 1; bench.py sends that to stderr, so
+    stdout holds exactly the one JSON line."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "bench.py", "--sharded", "--steps", "2", "--warmup", "1",
+           "--workload", "C_1024x131072", "--no-cpu-baseline", "--no-e2e", "--no-next-rows",
+           "--no-graph-probe", "--no-variants"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["rccl"]["nranks"] == 1 and out["parity"]["selected_set"] == "match"
