@@ -550,20 +550,28 @@ hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t
 //                  full-set kernel) and the score, written by the workgroup.
 // Bound: HBM -- each update's delta (C (d_in + 1) fp64) and its 2 nb gathered
 // samples are read once; the FMA work is 2 nb C d_in per update.
-constexpr int RB_ST = 8, RB_KC = 128, RB_KP = RB_KC + 4;
+// r4d: 512 threads and 16 samples per tile (Biscotti's batch of 10 is one
+// tile: one pass of the k-chains instead of two), the tile's sample indices
+// read once into LDS, and every staging load of a chunk issued before the
+// first LDS store (r4c staged one element per loop trip with the index load
+// and the sample load dependent in each: 160 us for 100 updates, 0.01 of HBM)
+constexpr int RB_NT = 512, RB_ST = 16, RB_KC = 128, RB_KP = RB_KC + 4;
+constexpr int RB_WPT = 2 * 16 * RB_KC / RB_NT;       // weight elements per thread (C <= 16)
+constexpr int RB_XPT = 2 * RB_ST * RB_KC / RB_NT;    // sample elements per thread
 
-__global__ __launch_bounds__(256) void k_roni_batch(const float *__restrict__ Xv, int64_t nv,
-                                                    int64_t din, int64_t ldv,
-                                                    const int32_t *__restrict__ yv, int C,
-                                                    const double *__restrict__ ww,
-                                                    const double *__restrict__ deltas, int64_t ld,
-                                                    const int64_t *__restrict__ idx, int64_t nb,
-                                                    double g, double *__restrict__ scores,
-                                                    int32_t *__restrict__ near_out) {
+__global__ __launch_bounds__(RB_NT) void k_roni_batch(const float *__restrict__ Xv, int64_t nv,
+                                                      int64_t din, int64_t ldv,
+                                                      const int32_t *__restrict__ yv, int C,
+                                                      const double *__restrict__ ww,
+                                                      const double *__restrict__ deltas, int64_t ld,
+                                                      const int64_t *__restrict__ idx, int64_t nb,
+                                                      double g, double *__restrict__ scores,
+                                                      int32_t *__restrict__ near_out) {
     __shared__ float xs[2][RB_ST][RB_KP];
     __shared__ float wsm[2][16][RB_KP];
     __shared__ float lgs[2][RB_ST][16];
     __shared__ double xnl[2][RB_ST], wnl[2][16], bl[2][16];
+    __shared__ int64_t srow[2][RB_ST];
     __shared__ unsigned int cnt[5];  // good0, good1, near0, near1, bad index
     const int tid = threadIdx.x;
     const int64_t j = blockIdx.x;
@@ -582,39 +590,90 @@ __global__ __launch_bounds__(256) void k_roni_batch(const float *__restrict__ Xv
     unsigned int good[2] = {0, 0}, near[2] = {0, 0};
     for (int64_t st0 = 0; st0 < nb; st0 += RB_ST) {
         const int ns = (int)(nb - st0 < RB_ST ? nb - st0 : RB_ST);
+        __syncthreads();  // the previous tile's rows and logits have been used
+        if (tid < 2 * RB_ST) {  // the tile's sample rows (padding repeats sample 0, never counted)
+            const int e = tid / RB_ST, s = tid - e * RB_ST;
+            int64_t row = ix[e * nb + st0 + (s < ns ? s : 0)];
+            if (row < 0 || row >= nv) {
+                cnt[4] = 1;  // reported as score NaN, near ties -1; never read out of range
+                row = 0;
+            }
+            srow[e][s] = row;
+        }
         double acc = 0.0, xacc = 0.0;  // logit (le, ls, lc); thread c == 0: |x_s|
+        double wa[RB_WPT], wb[RB_WPT];
+        float xv[RB_XPT];
+        // chunk k0's loads into registers (every load issued before any use)
+        auto load = [&](int64_t k0) {
+            const int kn = (int)(din - k0 < RB_KC ? din - k0 : RB_KC);
+#pragma unroll
+            for (int q = 0; q < RB_WPT; ++q) {
+                const int i = tid + RB_NT * q;
+                const int e = i / (16 * RB_KC), r = i - e * (16 * RB_KC), c = r / RB_KC,
+                          kk = r - c * RB_KC;
+                const bool on = c < C && kk < kn;
+                const int64_t wi = on ? (int64_t)c * din + k0 + kk : 0;
+                wa[q] = on ? ww[wi] : 0.0;
+                wb[q] = on && e == 1 ? dj[wi] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < RB_XPT; ++q) {
+                const int i = tid + RB_NT * q;
+                const int e = i / (RB_ST * RB_KC), r = i - e * (RB_ST * RB_KC), s = r / RB_KC,
+                          kk = r - s * RB_KC;
+                xv[q] = kk < kn ? Xv[srow[e][s] * ldv + k0 + kk] : 0.0f;
+            }
+        };
+        __syncthreads();  // srow is written
+        load(0);
         for (int64_t k0 = 0; k0 < din; k0 += RB_KC) {
             const int kn = (int)(din - k0 < RB_KC ? din - k0 : RB_KC);
             __syncthreads();  // the previous chunk has been consumed
-            for (int i = tid; i < 2 * C * RB_KC; i += 256) {
-                const int e = i / (C * RB_KC), r = i - e * (C * RB_KC), c = r / RB_KC,
+#pragma unroll
+            for (int q = 0; q < RB_WPT; ++q) {
+                const int i = tid + RB_NT * q;
+                const int e = i / (16 * RB_KC), r = i - e * (16 * RB_KC), c = r / RB_KC,
                           kk = r - c * RB_KC;
-                float w = 0.0f;
-                if (kk < kn) {
-                    const int64_t wi = (int64_t)c * din + k0 + kk;
-                    w = (float)(e == 0 ? ww[wi] : ww[wi] + dj[wi]);
-                }
-                wsm[e][c][kk] = w;
+                if (c < C) wsm[e][c][kk] = kk < kn ? (float)(e == 0 ? wa[q] : wa[q] + wb[q]) : 0.0f;
             }
-            for (int i = tid; i < 2 * RB_ST * RB_KC; i += 256) {
+#pragma unroll
+            for (int q = 0; q < RB_XPT; ++q) {
+                const int i = tid + RB_NT * q;
                 const int e = i / (RB_ST * RB_KC), r = i - e * (RB_ST * RB_KC), s = r / RB_KC,
                           kk = r - s * RB_KC;
-                const int ss = s < ns ? s : 0;  // padding rows repeat sample 0 (never counted)
-                int64_t row = ix[e * nb + st0 + ss];
-                if (row < 0 || row >= nv) {
-                    cnt[4] = 1;  // reported as score NaN, near ties -1; never read out of range
-                    row = 0;
-                }
-                xs[e][s][kk] = kk < kn ? Xv[row * ldv + k0 + kk] : 0.0f;
+                xs[e][s][kk] = xv[q];
             }
             __syncthreads();
+            // the next chunk's loads fly under this chunk's FMA chains
+            if (k0 + RB_KC < din) load(k0 + RB_KC);
             if (lt) {
                 const float *xr = xs[le][ls], *wr = wsm[le][lc];
-                for (int kk = 0; kk < kn; ++kk) {
+                const bool xn = lc == 0, wn = ls == 0 && st0 == 0;
+                // 16 columns at a time: their 8 LDS reads issued together, then
+                // the 16 FMAs of the chain in k order (r4c read 2 floats and
+                // waited for them before every FMA: ~100 cycles per step)
+                int kk = 0;
+                for (; kk + 16 <= kn; kk += 16) {
+                    typedef float f4 __attribute__((ext_vector_type(4)));
+                    f4 xq[4], wq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        xq[q] = *reinterpret_cast<const f4 *>(xr + kk + 4 * q);
+                        wq[q] = *reinterpret_cast<const f4 *>(wr + kk + 4 * q);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        const double x = (double)xq[u >> 2][u & 3], w = (double)wq[u >> 2][u & 3];
+                        acc = __builtin_fma(x, w, acc);
+                        if (xn) xacc += x * x;
+                        if (wn) wnacc += w * w;
+                    }
+                }
+                for (; kk < kn; ++kk) {
                     const double x = (double)xr[kk];
                     acc = __builtin_fma(x, (double)wr[kk], acc);
-                    if (lc == 0) xacc += x * x;
-                    if (ls == 0 && st0 == 0) wnacc += (double)wr[kk] * (double)wr[kk];
+                    if (xn) xacc += x * x;
+                    if (wn) wnacc += (double)wr[kk] * (double)wr[kk];
                 }
             }
         }
@@ -635,9 +694,7 @@ __global__ __launch_bounds__(256) void k_roni_batch(const float *__restrict__ Xv
                         best = c;
                         b0 = lg[c];
                     }
-                int64_t row = ix[e * nb + st0 + s];
-                row = row < 0 || row >= nv ? 0 : row;
-                good[e] += best == yv[row];
+                good[e] += best == yv[srow[e][s]];
                 near[e] += softmax_near_tie(lg, C, best, xnl[e][s], wnl[e], bl[e], g);
             }
         }
@@ -666,7 +723,7 @@ hipError_t launch_roni_softmax_batches(const float *Xv, int64_t nv, int64_t din,
                                        const double *deltas, int64_t n, int64_t ld,
                                        const int64_t *idx, int64_t nb, double *scores,
                                        int32_t *near_out, hipStream_t st) {
-    hipLaunchKernelGGL(k_roni_batch, dim3((unsigned)n), dim3(256), 0, st, Xv, nv, din, ldv, yv, C,
+    hipLaunchKernelGGL(k_roni_batch, dim3((unsigned)n), dim3(RB_NT), 0, st, Xv, nv, din, ldv, yv, C,
                        ww, deltas, ld, idx, nb, roni_softmax_g(din), scores, near_out);
     return hipGetLastError();
 }
