@@ -186,8 +186,18 @@ __global__ __launch_bounds__(256) void k_roni_xnorm(const float *__restrict__ Xv
         }
         __syncthreads();
         if (tid < 64) {
+            // 16 values read together, then added in k order (r4c read one and
+            // waited for it before every add of the chain)
             const int kn = (int)(din - k0 < 64 ? din - k0 : 64);
-            for (int kk = 0; kk < kn; ++kk) {
+            int kk = 0;
+            for (; kk + 16 <= kn; kk += 16) {
+                float v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = t[tid][kk + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) acc += (double)v[u] * (double)v[u];
+            }
+            for (; kk < kn; ++kk) {
                 const double v = (double)t[tid][kk];
                 acc += v * v;
             }
@@ -197,17 +207,48 @@ __global__ __launch_bounds__(256) void k_roni_xnorm(const float *__restrict__ Xv
 }
 
 // |w_col| of every model-class column of Wt (the fp32 weights widened), k in
-// order: the oracle's sequential sum.  Coalesced across columns.
+// order: the oracle's sequential sum.  A workgroup takes 64 columns: all 256
+// threads load a 64-row chunk of them (coalesced rows, every load in flight,
+// the next chunk's issued before this one is summed), thread c < 64 adds its
+// column's 64 values in k order from LDS.  (r4c: one thread per column
+// looping over k with a global load per add, 4 workgroups for 1,010 columns.)
 __global__ __launch_bounds__(256) void k_roni_wnorm(const double *__restrict__ Wt, int64_t ldl,
                                                     int64_t din, double *__restrict__ wn) {
-    const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (col >= ldl) return;
+    __shared__ double t[64][65];
+    const int tid = threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.x * 64;
+    const int cc = tid & 63, r0 = tid >> 6;
+    const int64_t col = c0 + cc < ldl ? c0 + cc : ldl - 1;
+    double v[16];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int64_t k = k0 + r0 + 4 * u;
+            v[u] = k < din ? Wt[k * ldl + col] : 0.0;
+        }
+    };
     double acc = 0.0;
-    for (int64_t k = 0; k < din; ++k) {
-        const double v = Wt[k * ldl + col];
-        acc += v * v;
+    load(0);
+    for (int64_t k0 = 0; k0 < din; k0 += 64) {
+        __syncthreads();  // the previous chunk has been summed
+#pragma unroll
+        for (int u = 0; u < 16; ++u) t[r0 + 4 * u][cc] = v[u];
+        __syncthreads();
+        if (k0 + 64 < din) load(k0 + 64);
+        if (tid < 64) {
+            const int kn = (int)(din - k0 < 64 ? din - k0 : 64);
+            int kk = 0;
+            for (; kk + 16 <= kn; kk += 16) {
+                double q[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) q[u] = t[kk + u][tid];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) acc += q[u] * q[u];
+            }
+            for (; kk < kn; ++kk) acc += t[kk][tid] * t[kk][tid];
+        }
     }
-    wn[col] = __builtin_sqrt(acc);
+    if (tid < 64 && c0 + tid < ldl) wn[c0 + tid] = __builtin_sqrt(acc);
 }
 
 constexpr int RG_MT = 64, RG_NT = 128, RG_LT = RG_NT + 1;
@@ -512,7 +553,7 @@ hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t
     hipLaunchKernelGGL(k_roni_mm_prep<true>, dim3((unsigned)(ldl / 64), (unsigned)((rows + 31) / 32)),
                        dim3(256), 0, st, ww, deltas, ld, din, C, nmod, ldl, rows, Wt, bt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_roni_wnorm, dim3((unsigned)((ldl + 255) / 256)), dim3(256), 0, st, Wt, ldl,
+    hipLaunchKernelGGL(k_roni_wnorm, dim3((unsigned)((ldl + 63) / 64)), dim3(256), 0, st, Wt, ldl,
                        din, wn);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int64_t nx64 = (nv + RG_MT - 1) / RG_MT, ny64 = ldl / RG_NT;
