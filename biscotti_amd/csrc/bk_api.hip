@@ -183,6 +183,7 @@ struct bk_ctx {
     int agreed_dtype = -1, agreed_det = -1;
     DevBuf status;
     int test_fail_exchange = 0;  // test knob BK_TEST_FAIL_BEFORE_EXCHANGE (bk_create)
+    int test_i8_enomem = 0;      // test knob BK_TEST_I8_ENOMEM: K1i8's workspace "fails" (bk_create)
     int64_t exchanges = 0;        // exchanges of the packed Gram (bk_comm_stats)
     double exchanged_bytes = 0;   // bytes each rank put into them
 };
@@ -421,14 +422,28 @@ int get_i8(bk_ctx *c, int64_t n, int64_t d, int es, bk_ctx::I8Cached **out) {
     return BK_OK;
 }
 
+// K1i8's layout and workspace for this call, or nullptr when the call does not
+// take K1i8 -- or cannot: its range partials take R times the packed upper
+// (~34 GB at n = 16,384, d = 1M fp32), and a batch the exact path can still
+// take is not refused for them, it runs exact (its record then carries no
+// int8 bound)
+bk_ctx::I8Cached *i8_prepared(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
+                              int64_t ld) {
+    if (!i8_now(c, dX, dtype, d, ld)) return nullptr;
+    const std::string keep = g_err;
+    bk_ctx::I8Cached *e = nullptr;
+    int st = c->test_i8_enomem ? BK_ENOMEM : get_i8(c, n, d, (int)esize(dtype), &e);
+    if (st == BK_OK) st = ensure(c->i8ws, i8_workspace(e->L));
+    if (st == BK_OK) return e;
+    (void)hipGetLastError();  // a failed hipMalloc must not surface at the next launch check
+    g_err = keep;
+    return nullptr;
+}
+
 // Everything stage_gram allocates (K1's plan tables and split-K slabs), so a
 // caller can learn of an allocation failure before it launches anything
 int prepare_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld) {
-    if (i8_now(c, dX, dtype, d, ld)) {
-        bk_ctx::I8Cached *e = nullptr;
-        CHK(get_i8(c, n, d, (int)esize(dtype), &e));
-        return ensure(c->i8ws, i8_workspace(e->L));
-    }
+    if (i8_prepared(c, dX, dtype, n, d, ld)) return BK_OK;
     if (use_v3(c, dX, dtype, ld)) {
         Plan3 *p3 = nullptr;
         CHK(get_plan3(c, n, d, v3_bk(dtype), &p3));
@@ -453,12 +468,9 @@ int poison_upper(bk_ctx *c, double *U, int64_t n) {
 // then the trailing pair {column count, columns on the fp32 MFMA}, bk_upper_elems)
 int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld,
                double *U, Plan &pl) {
-    if (i8_now(c, dX, dtype, d, ld)) {
+    if (bk_ctx::I8Cached *e = i8_prepared(c, dX, dtype, n, d, ld)) {
         // K1i8: digit slices + bound (k_slice), the int8 GEMM (k_gram), the
         // fixed-order sum of the range partials + the record (k_reduce)
-        bk_ctx::I8Cached *e = nullptr;
-        CHK(get_i8(c, n, d, (int)esize(dtype), &e));
-        CHK(ensure(c->i8ws, i8_workspace(e->L)));
         pl.n = (int)n;
         pl.d = d;
         pl.T = (int)((n + 63) / 64);
@@ -1152,6 +1164,7 @@ int bk_create(bk_ctx **out, int device) {
     }
     if (const char *v = getenv("BK_SMALL_CHECK_LINES")) c->small_check_lines = atoi(v) != 0;
     if (const char *v = getenv("BK_TEST_FAIL_BEFORE_EXCHANGE")) c->test_fail_exchange = atoi(v);
+    if (const char *v = getenv("BK_TEST_I8_ENOMEM")) c->test_i8_enomem = atoi(v) != 0;
     e = configure_kernels();
     if (e == hipSuccess) e = configure_aggregate_kernels();
     if (e == hipSuccess) e = configure_i8_kernels();

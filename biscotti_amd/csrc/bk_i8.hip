@@ -90,6 +90,11 @@ constexpr int64_t I8_CHUNK_STRIDE = BK_I8_BLOCKED ? 8192 : I8_KC;
 #endif
 constexpr int I8_LDS = I8_NSTAGE * I8_STAGE;       // 96 / 144 KiB
 constexpr int I8_RANGE_BYTES = 131072;             // a row's slice of one column range (i8_layout)
+// the exponent of a (row, range) slice holding a NaN or an infinity: its
+// digits are zero, k_gram_i8 writes NaN into every Gram element of that row
+// (so K2 scores it NaN and ranks it last, as the reference's NaN distances
+// do), and k_i8_bound's scale 2^e becomes +inf (the bound, a near tie)
+constexpr int I8_NONFINITE = 1 << 20;
 
 // ---------------------------------------------------------------------------
 // slicing: grid (npad rows, R ranges), 512 threads.  The range's row slice
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(NT) void k_i8_slice(const T *__restrict__ X, int64_
     int e = 0;
     if (fin && mx > 0.0) (void)frexp(mx, &e);
     if (tid == 0) {
-        es[(int64_t)i * R + r] = e;
+        es[(int64_t)i * R + r] = fin ? e : I8_NONFINITE;
         l1o[(int64_t)i * R + r] = fin ? l1 : __builtin_inf();
     }
     int8_t *s0 = S, *s1 = s0 + plane, *s2 = s1 + plane;
@@ -254,7 +259,9 @@ __global__ __launch_bounds__(I8_BOUND_NT) void k_i8_bound(const int *__restrict_
             if (lane == 0) {
                 const int64_t c1 = rb[r + 1] < d ? rb[r + 1] : d;
                 const double dr = (double)(c1 > rb[r] ? c1 - rb[r] : 0);
-                term[r - r0] = 0x1p-21 * (2.0 * smax * lmax + 2.03 * dr * smax * smax);
+                // scaled before the product: smax^2 alone overflows for rows near
+                // 2^512 whose Gram (and this bound) are finite
+                term[r - r0] = (0x1p-21 * smax) * (2.0 * lmax + 2.03 * dr * smax);
             }
         }
         __syncthreads();
@@ -483,7 +490,7 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                                  (double)acc[2][a][bb][e];
                 const int64_t u = (int64_t)bi * T64 - (int64_t)bi * (bi - 1) / 2 + (bj - bi);
                 part[((int64_t)r * ntile64 + u) * 4096 + (gi & 63) * 64 + (gj & 63)] =
-                    ldexp(v, ei + ej - 26);
+                    (ei == I8_NONFINITE || ej == I8_NONFINITE) ? __builtin_nan("") : ldexp(v, ei + ej - 26);
             }
         }
 }

@@ -58,3 +58,16 @@ def test_compact_line_keeps_every_config_and_fits(tmp_path):
     assert summ["B_mnist"]["host_over_h2d_ms"] == 0.02
     assert summ["E_4096x262144_fp32_i8_certified"]["reruns"] == 0
     assert json.load(open(path))["variants"]["C_1024x131072"]["filler"]  # the full record
+
+
+def test_launcher_refuses_fewer_gpus_than_rccl_ranks():
+    """`bench.py --gpus N` without WORLD_SIZE starts its own
+    ranks; with the RCCL exchange and fewer visible GPUs than N it returns a
+    non-zero status and launches nothing."""
+    sys.path.insert(0, REPO)
+    import argparse
+    import bench
+    a = argparse.Namespace(gpus=8, exchange="rccl")
+    assert bench.launch_ranks(a, argv=["--gpus", "8"], gpus_fn=lambda: 1) != 0
+    a = argparse.Namespace(gpus=2, exchange="host")
+    assert bench.launch_ranks(a, argv=["--gpus", "2"], gpus_fn=lambda: 0) != 0

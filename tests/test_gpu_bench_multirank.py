@@ -54,6 +54,46 @@ def test_bench_two_ranks_host_exchange(workload):
     assert out["value"] > 0 and out["ms_per_step"] > 0
 
 
+def test_bench_launches_its_own_ranks():
+    """a plain `python3 bench.py --gpus 2` (no torchrun, no
+    WORLD_SIZE) starts its own two ranks as a child torch.distributed.run and
+    relays rank 0's line: n_gpus 2, both ranks agree on the set, the shard's
+    golden matches, and every rank's K1 and exchange time per step are in the
+    line.  The host exchange lets the two ranks share the box's one GPU."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--exchange", "host", "--workload", "C_1024x131072", "--no-cpu-baseline", "--no-e2e",
+           "--no-next-rows", "--no-graph-probe", "--no-variants"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["parity"]["selected_set"] == "match", out["parity"]
+    rc = out["rccl"]
+    assert rc["nranks"] == 2 and rc["ranks_agree"], rc
+    assert [p["rank"] for p in rc["per_rank"]] == [0, 1]
+    assert all(p["k_gram_ms"] > 0 and p["exchange_ms"] > 0 for p in rc["per_rank"]), rc
+    assert rc["exchange_ms"] == max(p["exchange_ms"] for p in rc["per_rank"])
+    assert sum(p["d_local"] for p in rc["per_rank"]) == out["config"]["d"]
+
+
+def test_bench_refuses_more_rccl_ranks_than_gpus():
+    """With the RCCL exchange every rank needs its own GPU: `--gpus N` with
+    fewer visible GPUs exits non-zero instead of measuring one GPU."""
+    import torch
+    have = torch.cuda.device_count()
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", str(have + 1), "--steps", "2", "--warmup", "1",
+           "--workload", "C_1024x131072", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and not r.stdout.strip(), (r.returncode, r.stdout[-500:])
+    assert "visible" in r.stderr
+
+
 def test_bench_stdout_is_one_json_line_with_rccl():
     """The driver parses bench.py's stdout: with RCCL initialised (the sharded
     path at one rank, as every rank of the 8-GPU run initialises it) RCCL

@@ -227,6 +227,46 @@ def test_i8_nonfinite_is_a_near_tie(engine):
         engine.set_f32_mode(_lib.BK_F32_EXACT)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_i8_nonfinite_rows_are_never_selected(engine, oracle, dtype):
+    """a row holding a NaN or an infinity must not look
+    like the zero vector to the int8 Gram (its digits are zero).  Its Gram
+    elements are NaN, so it scores NaN and ranks last -- as the reference's
+    NaN / inf distances rank it (logistic_validator.py:59-63) -- and the
+    selection equals the oracle's; the bound is +inf (near tie)."""
+    from biscotti_amd.dist import unpack_upper
+    n, d, f = 300, 9000, 90
+    rng = np.random.default_rng(11)
+    X = (0.01 * rng.standard_normal((n, d))).astype(dtype)
+    X[17, 123] = np.inf   # one inf element
+    X[40] = np.nan        # a whole NaN row
+    X[41, 8999] = -np.inf  # in the last range
+    X[5] = 0.0            # the all-zero row a NaN row used to look like
+    mode_set = engine.set_f32_mode if dtype == np.float32 else engine.set_f64_mode
+    i8 = _lib.BK_F32_I8 if dtype == np.float32 else _lib.BK_F64_I8
+    tX = torch.from_numpy(X).cuda()
+    U = torch.empty(int(_lib.lib().bk_upper_elems(n)), dtype=torch.float64, device="cuda")
+    mode_set(i8)
+    try:
+        engine.gram_upper_ptr(tX.data_ptr(), _lib.BK_F32 if dtype == np.float32 else _lib.BK_F64,
+                              n, d, d, U.data_ptr())
+        engine.synchronize()
+        sel, sc, _ = engine.multikrum(X, f)
+        mg = engine.selection_margin()
+    finally:
+        mode_set(0)
+    G = unpack_upper(U.cpu().numpy(), n)
+    for r in (17, 40, 41):
+        assert np.all(np.isnan(G[r])) and np.all(np.isnan(G[:, r]))
+    ok = np.setdiff1d(np.arange(n), [17, 40, 41])
+    assert np.all(np.isfinite(G[np.ix_(ok, ok)]))
+    assert mg["near_tie"]
+    assert not {17, 40, 41} & set(sel.tolist())
+    assert np.all(np.isnan(sc[[17, 40, 41]]))
+    osel, osc, _ = oracle.krum(X, f)
+    assert np.array_equal(sel, osel)
+
+
 def test_i8_shard_records_sum(engine):
     """Two column shards on the int8 path: each record carries its own bound,
     and the exchange's sum (here: on the host) finishes like the whole batch."""
@@ -333,3 +373,27 @@ def test_f64_i8_error_within_the_bound(engine, n, d):
     err = float(np.max(np.abs(unpack_upper(out[_lib.BK_F64_I8], n) - unpack_upper(out[_lib.BK_F64_EXACT], n))))
     print("fp64 K1i8 n=%d d=%d: max err %.3e bound %.3e" % (n, d, err, E))
     assert err <= E
+
+
+def test_i8_workspace_failure_runs_exact(oracle, monkeypatch):
+    """when K1i8's workspace (R range partials of the packed upper)
+    cannot be allocated the call runs on the exact path instead of failing
+    with BK_ENOMEM (test knob BK_TEST_I8_ENOMEM, read at bk_create)."""
+    from biscotti_amd.dist import unpack_upper
+    from biscotti_amd.krum import Engine
+    monkeypatch.setenv("BK_TEST_I8_ENOMEM", "1")
+    eng = Engine(0)
+    monkeypatch.delenv("BK_TEST_I8_ENOMEM")
+    try:
+        rng = np.random.default_rng(12)
+        X = rng.standard_normal((300, 4000)).astype(np.float32)
+        got = _upper(eng, X, _lib.BK_F32_I8)
+        want = _upper(eng, X, _lib.BK_F32_EXACT)
+        assert got[-2] == 0.0  # no int8 bound: the exact path ran
+        assert np.array_equal(unpack_upper(got, 300), unpack_upper(want, 300))
+        eng.set_f32_mode(_lib.BK_F32_I8)
+        sel, _, _ = eng.multikrum(X, 90)
+        eng.set_f32_mode(_lib.BK_F32_EXACT)
+        assert np.array_equal(sel, oracle.krum(X, 90)[0])
+    finally:
+        eng.close()

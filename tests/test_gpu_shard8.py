@@ -1,0 +1,125 @@
+"""The 8-GPU forms of BASELINE configs D and E, pinned at full size on one GPU
+(VERDICT r4 item 2).
+
+SURVEY.md §8(e): rank r of an 8-rank job owns the column shard
+shard_bounds(d, 8, r), computes its packed partial Gram
+(bk_gram_upper_device), the exchange sums the eight records, and every rank
+finishes on the sum (bk_finish_device) and writes the mean of its own
+columns.  Here the eight shard records of the FULL batch are computed on the
+one GPU, summed in rank order on the device (the deterministic exchange's
+fixed order: ncclAllGather + a rank-order sum), finished once per shard, and
+the concatenated shard means and the selection are compared with the
+reference goldens (tests/golden/gen_goldens.py runs
+ML/code/logistic_validator.py:54-65 on the same batch):
+
+* D_512x1M_f153, fp64, on the exact fp64 MFMA and on K1i8 (fp64 rows);
+* E_4096x262144_fp32 on the exact path (fp32 widened onto the fp64 MFMA), the
+  fp32 MFMA and K1i8.
+
+The selection must equal the golden (these batches' boundary gaps clear every
+mode's bound: near_tie is False) and every shard's mean must be within the
+§8(d) bound.  The summed record carries the whole batch: its column count is
+d, its fp32-MFMA column count is d on the fp32 MFMA path, and on K1i8 its
+Gram bound e_G is the rank-order sum of the eight shards' bounds, bit for bit.
+"""
+import numpy as np
+import pytest
+
+import golden_util as GU
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from biscotti_amd import _lib  # noqa: E402
+
+SHARDS = 8
+
+
+def _batch(engine, name):
+    p = GU.C.case_params(name)
+    n, d = p["n"], p["d"]
+    f32 = p["dtype"] == "float32"
+    X = torch.empty((n, d), dtype=torch.float32 if f32 else torch.float64, device="cuda")
+    dt = _lib.BK_F32 if f32 else _lib.BK_F64
+    engine.synth_fill_ptr(X.data_ptr(), dt, n, d, d, 0, d, p["seed"], p["nbyz"], p["mu_scale"],
+                          p["byz_scale"], p["sigma"], p["flags"])
+    return X, dt, p
+
+
+def _set_mode(engine, dt, mode):
+    if dt == _lib.BK_F64:
+        engine.set_f64_mode({"exact": _lib.BK_F64_EXACT, "i8": _lib.BK_F64_I8}[mode])
+        engine.set_f32_mode(_lib.BK_F32_EXACT)
+    else:
+        engine.set_f32_mode({"exact": _lib.BK_F32_EXACT, "mfma": _lib.BK_F32_MFMA,
+                             "i8": _lib.BK_F32_I8}[mode])
+        engine.set_f64_mode(_lib.BK_F64_EXACT)
+
+
+CASES = [("D_512x1M_f153", "exact"), ("D_512x1M_f153", "i8"),
+         ("E_4096x262144_fp32", "exact"), ("E_4096x262144_fp32", "mfma"),
+         ("E_4096x262144_fp32", "i8")]
+
+
+@pytest.mark.parametrize("name,mode", [c for c in CASES if GU.have(c[0])])
+def test_eight_shard_records_finish_like_the_golden(engine, name, mode):
+    from biscotti_amd.dist import all_shards
+    X, dt, p = _batch(engine, name)
+    n, d, f = p["n"], p["d"], p["f"]
+    usz = int(_lib.lib().bk_upper_elems(n))
+    acc = torch.zeros(usz, dtype=torch.float64, device="cuda")
+    U = torch.empty(usz, dtype=torch.float64, device="cuda")
+    shards = all_shards(d, SHARDS)
+    recs = []
+    _set_mode(engine, dt, mode)
+    try:
+        for c0, dl in shards:  # rank order
+            Xs = X[:, c0:c0 + dl]
+            engine.gram_upper_ptr(Xs.data_ptr(), dt, n, dl, X.stride(0), U.data_ptr())
+            engine.synchronize()
+            recs.append(U[-4:].cpu().numpy().copy())
+            acc += U
+        torch.cuda.synchronize()
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        sc = torch.empty(n, dtype=torch.float64, device="cuda")
+        mean = torch.empty(d, dtype=torch.float64, device="cuda")
+        sels, margins = [], []
+        for c0, dl in shards:  # every rank's finish: same selection, its own columns' mean
+            Xs = X[:, c0:c0 + dl]
+            mv = mean[c0:c0 + dl]
+            engine.finish_ptr(acc.data_ptr(), Xs.data_ptr(), dt, n, dl, X.stride(0), f,
+                              sel.data_ptr(), sc.data_ptr(), mv.data_ptr())
+            engine.synchronize()
+            sels.append(sel.cpu().numpy().copy())
+            margins.append(engine.selection_margin())
+    finally:
+        _set_mode(engine, dt, "exact")
+    tail = acc[-4:].cpu().numpy()
+    # the record of the whole batch: d columns, on the fp32 MFMA all of them in
+    # "mfma" mode, and on K1i8 the rank-order sum of the shards' bounds
+    assert [r[0] for r in recs] == [float(dl) for _, dl in shards]
+    assert tail[0] == d
+    assert tail[1] == (d if mode == "mfma" else 0.0)
+    eg = 0.0
+    for r in recs:
+        eg += float(r[2])
+    assert tail[2] == eg
+    if mode == "i8":
+        assert all(r[2] > 0 for r in recs)
+    else:
+        assert eg == 0.0
+    g = GU.load(name)
+    for s in sels[1:]:
+        assert np.array_equal(s, sels[0])  # every rank selects the same set
+    mg = margins[0]
+    assert mg["d"] == d and all(m == mg for m in margins)
+    print("%s %s x%d: gap %.4g err_bound %.4g near_tie %s e_G %.4g"
+          % (name, mode, SHARDS, mg["gap"], mg["err_bound"], mg["near_tie"], eg))
+    assert not mg["near_tie"], mg
+    assert np.array_equal(sels[0], g["sel"])
+    scores = sc.cpu().numpy()
+    err = float(np.max(np.abs(scores - g["scores"])))
+    assert err <= mg["err_bound"] / 2 + 1e-9 * float(np.max(np.abs(g["scores"])))
+    GU.check_mean(mean.cpu().numpy(), g, GU.manifest()[name])
+    del X, acc, U, mean
+    torch.cuda.empty_cache()
