@@ -165,11 +165,14 @@ def cpu_baseline(w, target_s=10.0, target_1core_s=6.0):
     return out
 
 
-F32_MODES = {"exact": 0, "mfma": 1, "certified": 2, "i8": 3, "i8_certified": 4}  # bk_f32_mode
+F32_MODES = {"exact": 0, "mfma": 1, "certified": 2, "i8": 3, "i8_certified": 4,  # bk_f32_mode
+             "i8x2": 5, "i8x2_certified": 6}
+I8_MODE_NAMES = ("i8", "i8_certified", "i8x2", "i8x2_certified")
 # int8 MFMA dense peak (MI355X: 2x the bf16 rate, ~5 POPS; measured 4.90 on
 # v_mfma_i32_32x32x32_i8, profiles/r01/ubench_i8.log)
 PEAK_I8_TOPS = 5000.0
-I8_PRODUCTS = 6  # K1i8's digit products of weight >= 2^-26 (bk_i8.hip)
+I8_PRODUCTS = {"i8": 6, "i8_certified": 6,  # K1i8's digit products (bk_i8.hip): weight >= 2^-26
+               "i8x2": 3, "i8x2_certified": 3}  # two digits: weight >= 2^-19
 
 
 def gram_roofline(n, dl, k_ms, dtype, f32_mode, exact_rerun=False):
@@ -178,15 +181,15 @@ def gram_roofline(n, dl, k_ms, dtype, f32_mode, exact_rerun=False):
     MFMA (BK_F32_I8*: 6 digit products per Gram element; achieved in int8
     TOPS, plus the fp64-equivalent rate n(n+1) d / t)."""
     flops = n * (n + 1) * dl
-    i8 = f32_mode in ("i8", "i8_certified")  # fp32 rows (BK_F32_I8*) or fp64 rows (BK_F64_I8*)
+    i8 = f32_mode in I8_MODE_NAMES  # fp32 rows (BK_F32_I8*) or fp64 rows (BK_F64_I8*)
     mode = "exact" if exact_rerun or (dtype != "f32" and not i8) else f32_mode
-    if mode in ("i8", "i8_certified"):
-        ops = I8_PRODUCTS * flops
+    if mode in I8_MODE_NAMES:
+        ops = I8_PRODUCTS[mode] * flops
         ach = ops / (k_ms * 1e-3) / 1e12
         return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)",
                 "frac": round(ach / PEAK_I8_TOPS, 4), "ops_per_launch": ops,
                 "fp64_equiv_tflops": round(flops / (k_ms * 1e-3) / 1e12, 3),
-                "arithmetic": "int8 MFMA (6 exact digit products)"}
+                "arithmetic": "int8 MFMA (%d exact digit products)" % I8_PRODUCTS[mode]}
     peak = PEAK_TFLOPS["f32" if mode in ("mfma", "certified") else "f64"]
     ach = flops / (k_ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
@@ -280,9 +283,9 @@ def device_variant(eng, dev, name, f32_mode="exact", steps=20, warmup=5, X=None)
                             kernel_avg_ms=round(kt["avg_ms"], 4)),
            "step_roofline": {"t_floor_ms": round(t_floor, 4), "frac": round(t_floor / ms, 4)},
            "parity": par}
-    if f32_mode in ("certified", "i8_certified"):
+    if f32_mode in ("certified", "i8_certified", "i8x2_certified"):
         out["certified_reruns"] = reruns
-    if f32_mode in ("i8", "i8_certified"):
+    if f32_mode in I8_MODE_NAMES:
         kb = eng.timing_read()  # (cleared above) the slicing pass, evented once more
         eng.timing_select(["k_slice", "k_reduce"])
         set_mode(F32_MODES[f32_mode])
@@ -939,8 +942,8 @@ def main():
     eng = Engine(dev_idx)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     # fp64 rows take the int8 modes through bk_set_f64_mode (K1i8 for fp64 rows)
-    f64_i8 = w["dtype"] == "f64" and a.f32_mode in ("i8", "i8_certified")
-    if w["dtype"] == "f64" and a.f32_mode not in ("exact", "i8", "i8_certified"):
+    f64_i8 = w["dtype"] == "f64" and a.f32_mode in I8_MODE_NAMES
+    if w["dtype"] == "f64" and a.f32_mode not in ("exact",) + I8_MODE_NAMES:
         raise SystemExit("--f32-mode %s applies to fp32 rows only" % a.f32_mode)
     if f64_i8:
         eng.set_f64_mode(F32_MODES[a.f32_mode])
@@ -1225,8 +1228,8 @@ def main():
         # reference's -- an exact re-run on a near tie -- and K4 reads the fp64
         # rows).  A variant, never `value`: the headline stays the fp64 MFMA path
         V = out.setdefault("variants", {})
-        V[workload_tag(a.workload, "i8_certified")] = device_variant(
-            eng, dev, a.workload, "i8_certified", steps=20, X=X)
+        for mode in ("i8_certified", "i8x2_certified"):
+            V[workload_tag(a.workload, mode)] = device_variant(eng, dev, a.workload, mode, steps=20, X=X)
 
     if rank == 0 and world == 1 and not emu and not a.no_variants:
         # every other single-GPU BASELINE config in the driver-timed line, each
@@ -1245,7 +1248,7 @@ def main():
                 XE = torch.empty((we["n"], we["d"]), dtype=torch.float32, device=dev)
                 eng.synth_fill_ptr(XE.data_ptr(), _lib.BK_F32, we["n"], we["d"], we["d"], 0,
                                    we["d"], we["seed"], we["nbyz"])
-            for mode in ("exact", "mfma", "certified", "i8", "i8_certified"):
+            for mode in ("exact", "mfma", "certified") + I8_MODE_NAMES:
                 if a.workload == "E_4096x262144_fp32" and mode == a.f32_mode:
                     continue  # that is the line itself
                 V[workload_tag("E_4096x262144_fp32", mode)] = device_variant(

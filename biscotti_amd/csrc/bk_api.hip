@@ -382,26 +382,29 @@ bool f32_mfma_now(const bk_ctx *c, int dtype) {
 }
 
 // rows on the int8-sliced Gram (K1i8) for this call: fp32 rows under
-// BK_F32_I8 / BK_F32_I8_CERTIFIED, fp64 rows under BK_F64_I8 /
-// BK_F64_I8_CERTIFIED, outside a certified exact re-run; 16-B aligned rows, d >= 64
-bool i8_now(const bk_ctx *c, const void *dX, int dtype, int64_t d, int64_t ld) {
+// BK_F32_I8* / BK_F32_I8X2*, fp64 rows under BK_F64_I8* / BK_F64_I8X2*,
+// outside a certified exact re-run; 16-B aligned rows, d >= 64.  Returns the
+// digit count (3, or 2 for the X2 modes), 0 when the call runs elsewhere
+int i8_now(const bk_ctx *c, const void *dX, int dtype, int64_t d, int64_t ld) {
     const int mode = dtype == BK_F32 ? c->f32_mode : c->f64_mode;
     const int64_t epg = dtype == BK_F32 ? 4 : 2;
-    return !c->force_exact && d >= 64 && (ld % epg) == 0 && ((uintptr_t)dX % 16) == 0 &&
-           (mode == BK_F32_I8 || mode == BK_F32_I8_CERTIFIED);
+    if (c->force_exact || d < 64 || (ld % epg) != 0 || ((uintptr_t)dX % 16) != 0) return 0;
+    if (mode == BK_F32_I8 || mode == BK_F32_I8_CERTIFIED) return 3;
+    if (mode == BK_F32_I8X2 || mode == BK_F32_I8X2_CERTIFIED) return 2;
+    return 0;
 }
 
 // K1i8's layout (ranges, tile order) and its device tables, cached per (n, d)
-int get_i8(bk_ctx *c, int64_t n, int64_t d, int es, bk_ctx::I8Cached **out) {
+int get_i8(bk_ctx *c, int64_t n, int64_t d, int es, int ns, bk_ctx::I8Cached **out) {
     for (auto &e : c->i8)
-        if (e.n == n && e.d == d && e.L.es == es) {
+        if (e.n == n && e.d == d && e.L.es == es && e.L.ns == ns) {
             *out = &e;
             return BK_OK;
         }
     bk_ctx::I8Cached e;
     e.n = n;
     e.d = d;
-    e.L = i8_layout((int)n, d, es, c->num_cu);
+    e.L = i8_layout((int)n, d, es, c->num_cu, ns);
     const size_t tb = (size_t)(e.L.R + 1) * 8 + e.L.order.size() * sizeof(int);
     std::vector<char> h(tb);
     memcpy(h.data(), e.L.rb.data(), (size_t)(e.L.R + 1) * 8);
@@ -429,10 +432,11 @@ int get_i8(bk_ctx *c, int64_t n, int64_t d, int es, bk_ctx::I8Cached **out) {
 // int8 bound)
 bk_ctx::I8Cached *i8_prepared(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d,
                               int64_t ld) {
-    if (!i8_now(c, dX, dtype, d, ld)) return nullptr;
+    const int ns = i8_now(c, dX, dtype, d, ld);
+    if (!ns) return nullptr;
     const std::string keep = g_err;
     bk_ctx::I8Cached *e = nullptr;
-    int st = c->test_i8_enomem ? BK_ENOMEM : get_i8(c, n, d, (int)esize(dtype), &e);
+    int st = c->test_i8_enomem ? BK_ENOMEM : get_i8(c, n, d, (int)esize(dtype), ns, &e);
     if (st == BK_OK) st = ensure(c->i8ws, i8_workspace(e->L));
     if (st == BK_OK) return e;
     (void)hipGetLastError();  // a failed hipMalloc must not surface at the next launch check
@@ -1071,8 +1075,9 @@ struct DeviceGuard {
 };
 
 bool certified(const bk_ctx *c, int dtype) {
-    if (dtype == BK_F64) return c->f64_mode == BK_F64_I8_CERTIFIED;
-    return c->f32_mode == BK_F32_CERTIFIED || c->f32_mode == BK_F32_I8_CERTIFIED;
+    if (dtype == BK_F64) return c->f64_mode == BK_F64_I8_CERTIFIED || c->f64_mode == BK_F64_I8X2_CERTIFIED;
+    return c->f32_mode == BK_F32_CERTIFIED || c->f32_mode == BK_F32_I8_CERTIFIED ||
+           c->f32_mode == BK_F32_I8X2_CERTIFIED;
 }
 
 // BK_F32_CERTIFIED: run on the fp32 MFMA; if the selection margin does not
@@ -1366,7 +1371,7 @@ int bk_multikrum_device(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t
 
 int bk_set_f32_mode(bk_ctx *c, int mode) {
     if (!c) return fail(BK_EINVAL, "null context");
-    if (mode < BK_F32_EXACT || mode > BK_F32_I8_CERTIFIED)
+    if (mode < BK_F32_EXACT || mode > BK_F32_I8X2_CERTIFIED)
         return fail(BK_EINVAL, "bad f32 mode %d", mode);
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f32_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
@@ -1376,7 +1381,8 @@ int bk_set_f32_mode(bk_ctx *c, int mode) {
 
 int bk_set_f64_mode(bk_ctx *c, int mode) {
     if (!c) return fail(BK_EINVAL, "null context");
-    if (mode != BK_F64_EXACT && mode != BK_F64_I8 && mode != BK_F64_I8_CERTIFIED)
+    if (mode != BK_F64_EXACT && mode != BK_F64_I8 && mode != BK_F64_I8_CERTIFIED &&
+        mode != BK_F64_I8X2 && mode != BK_F64_I8X2_CERTIFIED)
         return fail(BK_EINVAL, "bad f64 mode %d", mode);
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f64_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in

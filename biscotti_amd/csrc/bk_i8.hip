@@ -44,6 +44,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "bk_internal.h"
@@ -58,14 +59,6 @@ constexpr int I8_TILE = 128, I8_KC = 64, I8_S = 3;
 constexpr int I8_PLANE = I8_TILE * I8_KC;          // one digit plane of one operand per stage: 8 KiB
 constexpr int I8_OPND = I8_S * I8_PLANE;           // 24 KiB
 constexpr int I8_STAGE = 2 * I8_OPND;              // 48 KiB
-// K1i8's operand pipeline (BK_I8_PIPE; A/B builds): 1 = LDS stores from
-// registers fetched one chunk ahead (2 stages), 3 = LDS-DMA (global_load_lds)
-// into a 3-stage ring, two chunks ahead.  (2, the register path two chunks
-// ahead, needs a second 48-register set: it spilled.)
-#ifndef BK_I8_PIPE
-#define BK_I8_PIPE 1
-#endif
-constexpr int I8_NSTAGE = BK_I8_PIPE == 3 ? 3 : 2;
 // digit-plane layout (A/B builds): 0 = row-major (row i's range at i * dp),
 // 1 = blocked per (row-block of 128, 64-column chunk): 8 KiB contiguous, so a
 // chunk fetch of a row-block is one 8-KiB run instead of 128 64-B pieces
@@ -88,7 +81,7 @@ constexpr int64_t I8_CHUNK_STRIDE = BK_I8_BLOCKED ? 8192 : I8_KC;
 #ifndef BK_I8_MAP
 #define BK_I8_MAP 1
 #endif
-constexpr int I8_LDS = I8_NSTAGE * I8_STAGE;       // 96 / 144 KiB
+constexpr int I8_LDS = 2 * I8_STAGE;               // 96 KiB: two stages
 constexpr int I8_RANGE_BYTES = 131072;             // a row's slice of one column range (i8_layout)
 // the exponent of a (row, range) slice holding a NaN or an infinity: its
 // digits are zero, k_gram_i8 writes NaN into every Gram element of that row
@@ -112,7 +105,9 @@ constexpr int I8_NONFINITE = 1 << 20;
 // ranges: config E's 8-rank shard has 4,096 per range), where 512 threads
 // would leave half idle and every register block but one unused
 constexpr int I8_SLICE_NT = 512;
-template <typename T, int NT = I8_SLICE_NT,
+// NS: digit planes written (3, or 2 for BK_F32_I8X2: x / s = a0/64 + a1/2^13 + rho,
+// |rho| <= 2^-14)
+template <typename T, int NS, int NT = I8_SLICE_NT,
           int MAXU = I8_RANGE_BYTES / (int)(sizeof(T) * 16 * I8_SLICE_NT)>
 __global__ __launch_bounds__(NT) void k_i8_slice(const T *__restrict__ X, int64_t ld, int n,
                                                  int64_t d, const int64_t *__restrict__ rb, int R,
@@ -194,7 +189,7 @@ __global__ __launch_bounds__(NT) void k_i8_slice(const T *__restrict__ X, int64_
         es[(int64_t)i * R + r] = fin ? e : I8_NONFINITE;
         l1o[(int64_t)i * R + r] = fin ? l1 : __builtin_inf();
     }
-    int8_t *s0 = S, *s1 = s0 + plane, *s2 = s1 + plane;
+    int8_t *s0 = S, *s1 = s0 + plane, *s2 = s1 + plane;  // (s2: three digits only)
 #pragma unroll
     for (int u = 0; u < MAXU; ++u) {
         const int c = u * BLK + 16 * tid;
@@ -210,10 +205,12 @@ __global__ __launch_bounds__(NT) void k_i8_slice(const T *__restrict__ X, int64_
                 const double a0 = __builtin_rint(y);
                 const double y1 = (y - a0) * 128.0;  // exact
                 const double a1 = __builtin_rint(y1);
-                const double a2 = __builtin_rint((y1 - a1) * 128.0);
                 p0 |= ((int)a0 & 0xff) << (8 * w);
                 p1 |= ((int)a1 & 0xff) << (8 * w);
-                p2 |= ((int)a2 & 0xff) << (8 * w);
+                if constexpr (NS == 3) {
+                    const double a2 = __builtin_rint((y1 - a1) * 128.0);
+                    p2 |= ((int)a2 & 0xff) << (8 * w);
+                }
             }
             dig[0][q] = p0;
             dig[1][q] = p1;
@@ -222,7 +219,8 @@ __global__ __launch_bounds__(NT) void k_i8_slice(const T *__restrict__ X, int64_
         const int64_t o = i8_off(i, c0 + c, dp);
         *reinterpret_cast<v4i *>(s0 + o) = v4i{dig[0][0], dig[0][1], dig[0][2], dig[0][3]};
         *reinterpret_cast<v4i *>(s1 + o) = v4i{dig[1][0], dig[1][1], dig[1][2], dig[1][3]};
-        *reinterpret_cast<v4i *>(s2 + o) = v4i{dig[2][0], dig[2][1], dig[2][2], dig[2][3]};
+        if constexpr (NS == 3)
+            *reinterpret_cast<v4i *>(s2 + o) = v4i{dig[2][0], dig[2][1], dig[2][2], dig[2][3]};
     }
 }
 
@@ -236,7 +234,7 @@ constexpr int I8_BOUND_NT = 1024, I8_BOUND_BATCH = 1024;
 __global__ __launch_bounds__(I8_BOUND_NT) void k_i8_bound(const int *__restrict__ es,
                                                           const double *__restrict__ l1,
                                                           const int64_t *__restrict__ rb, int R, int n,
-                                                          int64_t d, double *__restrict__ out) {
+                                                          int64_t d, int ns, double *__restrict__ out) {
     __shared__ double term[I8_BOUND_BATCH];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double tot = 0.0;
@@ -260,8 +258,12 @@ __global__ __launch_bounds__(I8_BOUND_NT) void k_i8_bound(const int *__restrict_
                 const int64_t c1 = rb[r + 1] < d ? rb[r + 1] : d;
                 const double dr = (double)(c1 > rb[r] ? c1 - rb[r] : 0);
                 // scaled before the product: smax^2 alone overflows for rows near
-                // 2^512 whose Gram (and this bound) are finite
-                term[r - r0] = (0x1p-21 * smax) * (2.0 * lmax + 2.03 * dr * smax);
+                // 2^512 whose Gram (and this bound) are finite.  Three digits:
+                // 2^-21 (2 S L1 + 2.03 d S^2); two digits (three products):
+                // 2^-14 (2 S L1 + 1.0001 d S^2) -- the dropped a1 b1 2^-26 term
+                // and the remainders rho (|rho| <= 2^-14), DESIGN.md §4 K1i8
+                term[r - r0] = ns == 3 ? (0x1p-21 * smax) * (2.0 * lmax + 2.03 * dr * smax)
+                                       : (0x1p-14 * smax) * (2.0 * lmax + 1.0001 * dr * smax);
             }
         }
         __syncthreads();
@@ -274,38 +276,68 @@ __global__ __launch_bounds__(I8_BOUND_NT) void k_i8_bound(const int *__restrict_
 }
 
 // ---------------------------------------------------------------------------
-// the int8 Gram: one 128 x 128 tile of one range per workgroup
+// the int8 Gram: one 128 x TJ tile of one range per workgroup
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int i8_swz(int row, int g) { return g ^ ((row >> 2) & 3); }
 
+// NS digit planes, NBJ 32-column blocks per wave along the tile's columns:
+//   <3, 2>  128 x 128 tiles, the six products of weight >= 2^-26 (three
+//           accumulator levels, 192 int32 per lane)
+//   <2, 4>  128 x 256 tiles, the three products of weight >= 2^-19
+//           (BK_F32_I8X2: L0 = A0 A0^T, L1 = A0 A1^T + A1 A0^T; two levels,
+//           256 int32 per lane)
+// Both stage 48 KiB per 64-column chunk (NS (128 + TJ) rows of 64 B) and run
+// 24 MFMAs against 12 fragment reads per 32-column k-step and wave, so the
+// two-digit tile does the same instruction stream per chunk for twice the
+// output elements and half the products each.
+template <int NS, int NBJ>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                const int64_t *__restrict__ rb, int R, const int2 *__restrict__ order,
                const int *__restrict__ es, int n, int T64, double *__restrict__ part,
                int64_t ntile64) {
+    constexpr int TJ = 64 * NBJ;                       // the tile's columns (rows of operand B)
+    constexpr int NL = NS;                             // accumulator levels
+    constexpr int NP = NS == 3 ? 6 : 3;                // digit products
+    constexpr int A_BYTES = NS * I8_TILE * I8_KC;      // operand A (the tile's rows) per stage
+    constexpr int B_PLANE = TJ * I8_KC;
+    static_assert(A_BYTES + NS * B_PLANE == I8_STAGE, "48 KiB stages");
+    static_assert(NP * 2 * NBJ == 24 && NS * (2 + NBJ) == 12, "24 MFMAs per 12 reads");
     extern __shared__ __attribute__((aligned(16))) int8_t lds[];  // two stages of I8_STAGE bytes
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // this workgroup's item: its 128-row tile (I | J << 16) and column range
-    // (i8_layout; r < 0: a padding workgroup of a short XCD list)
+    // this workgroup's item: its tile (row block I of 128, column block J of
+    // TJ: I | J << 16) and column range (i8_layout; r < 0: a padding workgroup
+    // of a short XCD list)
     const int2 item = order[blockIdx.x];
     if (item.y < 0) return;
     const int r = item.y, I = item.x & 0xffff, J = item.x >> 16;
     const int64_t k0 = rb[r], k1 = rb[r + 1];
     const int nch = (int)((k1 - k0) / I8_KC);
-#if BK_I8_PIPE == 1
-    // staging: granule (operand o, digit t, row, g) of the chunk; thread t
-    // moves 12: index q = tid + 256 u -> g = q & 3, row = (q >> 2) & 127,
-    // t = (q >> 9) % 3, o = q / 1536
+    // staging: granule q = tid + 256 u (u < 12) of the chunk: q < 512 NS is
+    // operand A (digit q >> 9, row (q >> 2) & 127), the rest operand B (digit
+    // q' / (4 TJ), row (q' >> 2) % TJ); g = q & 3 the 16-B granule of the row
     const int8_t *src[12];
     int dst[12];
 #pragma unroll
     for (int u = 0; u < 12; ++u) {
         const int q = tid + 256 * u;
-        const int g = q & 3, row = (q >> 2) & 127, t = (q >> 9) % 3, o = q / 1536;
-        const int grow = (o == 0 ? I : J) * I8_TILE + row;
+        const int g = q & 3;
+        int t, row, grow, off;
+        if (q < 512 * NS) {
+            t = q >> 9;
+            row = (q >> 2) & 127;
+            grow = I * I8_TILE + row;
+            off = t * I8_TILE * I8_KC;
+        } else {
+            const int qb = q - 512 * NS;
+            t = qb / (4 * TJ);
+            row = (qb >> 2) % TJ;
+            grow = J * TJ + row;
+            off = A_BYTES + t * B_PLANE;
+        }
         src[u] = S + (int64_t)t * plane + i8_off(grow, k0 + 16 * g, dp);
-        dst[u] = o * I8_OPND + t * I8_PLANE + row * I8_KC + 16 * i8_swz(row, g);
+        dst[u] = off + row * I8_KC + 16 * i8_swz(row, g);
     }
     v4i pf[12];
     auto fetch = [&](int ch) {
@@ -316,42 +348,45 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
 #pragma unroll
         for (int u = 0; u < 12; ++u) *reinterpret_cast<v4i *>(b + dst[u]) = pf[u];
     };
-#endif
-    v16i acc[3][2][2];
+    v16i acc[NL][2][NBJ];
 #pragma unroll
-    for (int l = 0; l < 3; ++l)
+    for (int l = 0; l < NL; ++l)
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) acc[l][a][b] = v16i{};
-    const int wr = (wave & 1) * 64, wc = (wave >> 1) * 64;
+            for (int b = 0; b < NBJ; ++b) acc[l][a][b] = v16i{};
+    const int wr = (wave & 1) * 64, wc = (wave >> 1) * (32 * NBJ);
     const int fr = lane & 31, fh = lane >> 5;
     // the fragments of k-step ks (32 columns: granules 2 ks + fh) of stage b
-    auto frags = [&](const int8_t *b, int ks, v4i (&fa)[3][2], v4i (&fb)[3][2]) {
+    auto frags = [&](const int8_t *b, int ks, v4i (&fa)[NS][2], v4i (&fb)[NS][NBJ]) {
         const int g = 2 * ks + fh;
 #pragma unroll
-        for (int t = 0; t < 3; ++t)
+        for (int t = 0; t < NS; ++t) {
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
-                const int ra = wr + 32 * a + fr, rbw = wc + 32 * a + fr;
-                fa[t][a] = *reinterpret_cast<const v4i *>(b + t * I8_PLANE + ra * I8_KC + 16 * i8_swz(ra, g));
-                fb[t][a] = *reinterpret_cast<const v4i *>(b + I8_OPND + t * I8_PLANE + rbw * I8_KC +
-                                                          16 * i8_swz(rbw, g));
+                const int ra = wr + 32 * a + fr;
+                fa[t][a] = *reinterpret_cast<const v4i *>(b + t * I8_TILE * I8_KC + ra * I8_KC +
+                                                          16 * i8_swz(ra, g));
             }
+#pragma unroll
+            for (int bb = 0; bb < NBJ; ++bb) {
+                const int rbw = wc + 32 * bb + fr;
+                fb[t][bb] = *reinterpret_cast<const v4i *>(b + A_BYTES + t * B_PLANE + rbw * I8_KC +
+                                                           16 * i8_swz(rbw, g));
+            }
+        }
     };
-    // the six digit products of one k-step, product-major over the 2 x 2
-    // blocks: consecutive MFMAs never accumulate into the same registers (a
-    // block's L1 and L2 chains are 4 MFMAs apart).  Measured neutral against
-    // block-major chains (13.55 vs 13.60 ms at config E): the 32x32x32 MFMA
-    // forwards its own accumulator, as the guide says of the bf16 form
-    auto mma = [&](const v4i (&fa)[3][2], const v4i (&fb)[3][2]) {
+    // the digit products of one k-step {level, A digit, B digit}, product-major
+    // over the blocks: consecutive MFMAs never accumulate into the same
+    // registers.  (Measured neutral against block-major chains at config E.)
+    auto mma = [&](const v4i (&fa)[NS][2], const v4i (&fb)[NS][NBJ]) {
         constexpr int PT[6][3] = {{0, 0, 0}, {1, 0, 1}, {1, 1, 0}, {2, 0, 2}, {2, 1, 1}, {2, 2, 0}};
 #pragma unroll
-        for (int p = 0; p < 6; ++p)
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int bb = 0; bb < 2; ++bb)
+                for (int bb = 0; bb < NBJ; ++bb)
                     acc[PT[p][0]][a][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
                         fa[PT[p][1]][a], fb[PT[p][2]][bb], acc[PT[p][0]][a][bb], 0, 0, 0);
     };
@@ -366,9 +401,8 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
     //            chunk ch's stage, chunk ch + 3 fetched
     // Chunk indices past the range are clamped (a stage nobody reads again
     // gets a stale copy; the last chunk is fetched again): no branch.
-#if BK_I8_PIPE == 1
     if (nch > 0) {
-        v4i F0a[3][2], F0b[3][2], F1a[3][2], F1b[3][2];
+        v4i F0a[NS][2], F0b[NS][NBJ], F1a[NS][2], F1b[NS][NBJ];
         const auto cl = [&](int c) { return c < nch ? c : nch - 1; };
         fetch(0);
         put(lds);
@@ -408,76 +442,13 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
         for (int ch = 0; ch < nch; ++ch)
             body(ch, lds + (ch & 1) * I8_STAGE, lds + ((ch + 1) & 1) * I8_STAGE);
     }
-#else
-    // LDS-DMA: wave w moves 1-KiB pieces q = 12 w + u (u < 12) of each chunk:
-    // piece q is 16 rows of one (operand, digit) plane, lane l landing at
-    // q KiB + 16 l = row (l >> 2), slot l & 3, whose source granule is the
-    // slot un-swizzled.  Chunk c lives in stage c % 3 and is issued at chunk
-    // c - 2's phase A; a wave waits for its own pieces (vmcnt), the barrier
-    // for everyone's.
-    if (nch > 0) {
-        v4i F0a[3][2], F0b[3][2], F1a[3][2], F1b[3][2];
-        const auto cl = [&](int c) { return c < nch ? c : nch - 1; };
-        const int8_t *dsrc[12];
-#pragma unroll
-        for (int u = 0; u < 12; ++u) {
-            const int q = 12 * wave + u;
-            const int o = q / 24, t = (q >> 3) % 3, row = 16 * (q & 7) + (lane >> 2);
-            const int g = (lane & 3) ^ ((row >> 2) & 3);
-            const int grow = (o == 0 ? I : J) * I8_TILE + row;
-            dsrc[u] = S + (int64_t)t * plane + i8_off(grow, k0 + 16 * g, dp);
-        }
-        auto dma = [&](int ch, int8_t *b) {
-#pragma unroll
-            for (int u = 0; u < 12; ++u)
-                __builtin_amdgcn_global_load_lds((const void *)(dsrc[u] + (int64_t)ch * I8_CHUNK_STRIDE),
-                                                 (void *)(b + (12 * wave + u) * 1024), 16, 0, 0);
-        };
-        dma(0, lds);
-        dma(cl(1), lds + I8_STAGE);
-        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        __syncthreads();
-        frags(lds, 0, F0a, F0b);
-        // restrict: the three stages never overlap (C and N read, F written)
-        auto body = [&](int ch, const int8_t *__restrict__ C, const int8_t *__restrict__ N,
-                        int8_t *__restrict__ F) {
-            mma(F0a, F0b);
-            frags(C, 1, F1a, F1b);
-            dma(cl(ch + 2), F);
-#pragma unroll
-            for (int k = 0; k < 12; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (the LDS-DMA piece)
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // chunk ch + 1's pieces
-            __syncthreads();
-            mma(F1a, F1b);
-            frags(N, 0, F0a, F0b);
-#pragma unroll
-            for (int k = 0; k < 12; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        for (int ch = 0; ch < nch; ++ch) {
-            const int sc = ch % 3;
-            body(ch, lds + sc * I8_STAGE, lds + (sc == 2 ? 0 : sc + 1) * I8_STAGE,
-                 lds + (sc == 0 ? 2 : sc - 1) * I8_STAGE);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
-    }
-#endif
-    // epilogue: C/D lane l, reg e of a 32 x 32 block: row (e & 3) + 8 (e >> 2) + 4 (l >> 5), col l & 31
+    // epilogue: C/D lane l, reg e of a 32 x 32 block: row (e & 3) + 8 (e >> 2) + 4 (l >> 5), col l & 31.
+    // Three digits: G = s_i s_j 2^-26 (2^14 L0 + 2^7 L1 + L2); two: s_i s_j 2^-19 (2^7 L0 + L1)
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            const int gj = J * I8_TILE + wc + 32 * bb + fr;
+        for (int bb = 0; bb < NBJ; ++bb) {
+            const int gj = J * TJ + wc + 32 * bb + fr;
             const int bj = gj >> 6;
             const int ej = gj < n ? es[(int64_t)gj * R + r] : 0;
 #pragma unroll
@@ -486,11 +457,19 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                 const int bi = gi >> 6;
                 if (bi > bj || bj >= T64) continue;  // the lower half of a diagonal tile; padding
                 const int ei = gi < n ? es[(int64_t)gi * R + r] : 0;
-                const double v = (double)acc[0][a][bb][e] * 16384.0 + (double)acc[1][a][bb][e] * 128.0 +
-                                 (double)acc[2][a][bb][e];
+                double v;
+                int sh;
+                if constexpr (NS == 3) {
+                    v = (double)acc[0][a][bb][e] * 16384.0 + (double)acc[1][a][bb][e] * 128.0 +
+                        (double)acc[2][a][bb][e];
+                    sh = -26;
+                } else {
+                    v = (double)acc[0][a][bb][e] * 128.0 + (double)acc[1][a][bb][e];
+                    sh = -19;
+                }
                 const int64_t u = (int64_t)bi * T64 - (int64_t)bi * (bi - 1) / 2 + (bj - bi);
                 part[((int64_t)r * ntile64 + u) * 4096 + (gi & 63) * 64 + (gj & 63)] =
-                    (ei == I8_NONFINITE || ej == I8_NONFINITE) ? __builtin_nan("") : ldexp(v, ei + ej - 26);
+                    (ei == I8_NONFINITE || ej == I8_NONFINITE) ? __builtin_nan("") : ldexp(v, ei + ej + sh);
             }
         }
 }
@@ -528,18 +507,31 @@ __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ pa
 // short of full, R is raised (in eights, up to 4x, ranges >= 16 chunks) to the
 // count that fills the rounds (config D: 10 tiles x 64 ranges = 2.5 rounds of
 // 32 CUs per XCD -> 128 ranges, 5 rounds; config E stays at 8: 16.5 of 17)
-I8Layout i8_layout(int n, int64_t d, int es, int num_cu) {
+I8Layout i8_layout(int n, int64_t d, int es, int num_cu, int ns) {
     I8Layout L;
-    L.npad = (n + I8_TILE - 1) / I8_TILE * I8_TILE;
+    L.ns = ns == 2 ? 2 : 3;
+    L.tj = L.ns == 2 ? 256 : I8_TILE;  // k_gram_i8<2, 4>: 128 x 256 tiles
+    L.npad = (n + L.tj - 1) / L.tj * L.tj;
     L.dp = (d + I8_KC - 1) / I8_KC * I8_KC;
     const int64_t nk = L.dp / I8_KC;
     const int64_t cmax = I8_RANGE_BYTES / es;  // columns per range
+    // the output tiles: row block I of 128, column block J of tj, every tile
+    // holding some element of the upper triangle (128 I <= tj J + tj - 1) and
+    // no tile past the last row; super-blocked (4 row blocks x 512 columns,
+    // row by row) so consecutive tiles share row blocks
+    const int TI = (n + I8_TILE - 1) / I8_TILE, TJn = (n + L.tj - 1) / L.tj, rj = L.tj / I8_TILE;
+    const int SBI = 4, SBJ = 4 / rj;
+    std::vector<int> tiles;  // I | J << 16
+    for (int BI = 0; BI < (TI + SBI - 1) / SBI; ++BI)
+        for (int BJ = 0; BJ < (TJn + SBJ - 1) / SBJ; ++BJ)
+            for (int I = BI * SBI; I < BI * SBI + SBI && I < TI; ++I)
+                for (int J = BJ * SBJ; J < BJ * SBJ + SBJ && J < TJn; ++J)
+                    if (I <= rj * J + rj - 1) tiles.push_back(I | J << 16);
+    const int NT = (int)tiles.size();
     int64_t R = (L.dp + cmax - 1) / cmax;
     R = (R + 7) / 8 * 8;
     R = nk < R ? nk : R;
     {
-        const int T = L.npad / I8_TILE;
-        const int64_t NT = (int64_t)T * (T + 1) / 2;
         const double cx = num_cu > 0 ? num_cu / 8.0 : 32.0;  // CUs per XCD
         auto eff = [&](int64_t r) {
             const double rounds = (double)((NT * r + 7) / 8) / cx;
@@ -558,17 +550,6 @@ I8Layout i8_layout(int n, int64_t d, int es, int num_cu) {
     L.T128 = L.npad / I8_TILE;
     L.T64 = (n + 63) / 64;
     L.ntile64 = (int64_t)L.T64 * (L.T64 + 1) / 2;
-    // super-blocked upper-triangle order of the 128-row tiles: blocks of 4 x 4
-    // tiles row by row, so consecutive tiles share row-blocks
-    constexpr int SB = 4;
-    const int T = L.T128, NB = (T + SB - 1) / SB;
-    std::vector<int> tiles;  // I | J << 16
-    for (int BI = 0; BI < NB; ++BI)
-        for (int BJ = BI; BJ < NB; ++BJ)
-            for (int I = BI * SB; I < BI * SB + SB && I < T; ++I)
-                for (int J = BJ * SB; J < BJ * SB + SB && J < T; ++J)
-                    if (I <= J) tiles.push_back(I | J << 16);
-    const int NT = (int)tiles.size();
 #if BK_I8_MAP == 0
     // r3/r4a: workgroup b runs range b mod R (= its XCD when R = 8) and tile b / R
     for (int b = 0; b < NT * L.R; ++b) {
@@ -609,13 +590,16 @@ I8Layout i8_layout(int n, int64_t d, int es, int num_cu) {
 
 size_t i8_workspace(const I8Layout &L) {
     // digit planes, rb, order, exponents, norms, bound, range partials
-    return (size_t)I8_S * L.plane + 256 + (size_t)(L.R + 1) * 8 + L.order.size() * 4 + 256 +
+    return (size_t)L.ns * L.plane + 256 + (size_t)(L.R + 1) * 8 + L.order.size() * 4 + 256 +
            (size_t)L.npad * L.R * (4 + 8) + 256 + 256 +
            (size_t)L.R * L.ntile64 * 4096 * 8 + 256;
 }
 
 hipError_t configure_i8_kernels() {
-    return hipFuncSetAttribute((const void *)k_gram_i8, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void *)k_gram_i8<3, 2>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, I8_LDS);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void *)k_gram_i8<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                I8_LDS);
 }
 
@@ -631,7 +615,7 @@ static I8Ws i8_ws(const I8Layout &L, void *ws) {
     I8Ws w;
     char *p = align256((char *)ws);
     w.S = (int8_t *)p;
-    p = align256(p + (size_t)I8_S * L.plane);
+    p = align256(p + (size_t)L.ns * L.plane);
     w.es = (int *)p;
     p = align256(p + (size_t)L.npad * L.R * 4);
     w.l1 = (double *)p;
@@ -651,21 +635,30 @@ hipError_t launch_i8_slice(const void *X, int dtype, int64_t ld, int n, int64_t 
     if (lmax * L.es > I8_RANGE_BYTES) return hipErrorInvalidValue;
     const dim3 grid((unsigned)L.npad, (unsigned)L.R);
     const bool shortr = lmax <= 16 * 256;  // every range fits <256, 1>
-    if (dtype == 0 && shortr)
-        hipLaunchKernelGGL((k_i8_slice<double, 256, 1>), grid, dim3(256), 0, st, (const double *)X, ld,
-                           n, d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+    auto go = [&](auto tag, auto ns) {
+        using T = decltype(tag);
+        constexpr int NS = decltype(ns)::value;
+        if (shortr)
+            hipLaunchKernelGGL((k_i8_slice<T, NS, 256, 1>), grid, dim3(256), 0, st, (const T *)X, ld, n,
+                               d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+        else
+            hipLaunchKernelGGL((k_i8_slice<T, NS>), grid, dim3(I8_SLICE_NT), 0, st, (const T *)X, ld, n,
+                               d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+    };
+    using N2 = std::integral_constant<int, 2>;
+    using N3 = std::integral_constant<int, 3>;
+    if (dtype == 0 && L.ns == 2)
+        go(double{}, N2{});
     else if (dtype == 0)
-        hipLaunchKernelGGL(k_i8_slice<double>, grid, dim3(I8_SLICE_NT), 0, st, (const double *)X, ld, n,
-                           d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
-    else if (shortr)
-        hipLaunchKernelGGL((k_i8_slice<float, 256, 1>), grid, dim3(256), 0, st, (const float *)X, ld, n,
-                           d, rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+        go(double{}, N3{});
+    else if (L.ns == 2)
+        go(float{}, N2{});
     else
-        hipLaunchKernelGGL(k_i8_slice<float>, grid, dim3(I8_SLICE_NT), 0, st, (const float *)X, ld, n, d,
-                           rb, L.R, w.S, L.dp, L.plane, w.es, w.l1);
+        go(float{}, N3{});
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_i8_bound, dim3(1), dim3(I8_BOUND_NT), 0, st, w.es, w.l1, rb, L.R, n, d, w.bound);
+    hipLaunchKernelGGL(k_i8_bound, dim3(1), dim3(I8_BOUND_NT), 0, st, w.es, w.l1, rb, L.R, n, d, L.ns,
+                       w.bound);
     return hipGetLastError();
 }
 
@@ -674,8 +667,12 @@ hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables
     const int64_t *rb = (const int64_t *)tables;  // {rb (R + 1 int64), order (int pairs)}
     const int2 *order = (const int2 *)((const char *)tables + (size_t)(L.R + 1) * 8);
     const int64_t items = (int64_t)L.order.size() / 2;  // one workgroup each
-    hipLaunchKernelGGL(k_gram_i8, dim3((unsigned)items), dim3(256), I8_LDS, st, w.S, L.dp,
-                       L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
+    if (L.ns == 2)
+        hipLaunchKernelGGL((k_gram_i8<2, 4>), dim3((unsigned)items), dim3(256), I8_LDS, st, w.S, L.dp,
+                           L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
+    else
+        hipLaunchKernelGGL((k_gram_i8<3, 2>), dim3((unsigned)items), dim3(256), I8_LDS, st, w.S, L.dp,
+                           L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
     return hipGetLastError();
 }
 

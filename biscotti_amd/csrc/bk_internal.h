@@ -177,12 +177,14 @@ hipError_t launch_roni_softmax_batches(const float *Xv, int64_t nv, int64_t din,
 // bk_i8.hip: K1i8, the Gram of fp32 rows from exact int8 digit slices
 // (BK_F32_I8): column ranges (one per XCD), digit planes [3][npad][dp] int8
 struct I8Layout {
-    int npad = 0, R = 0, T128 = 0, T64 = 0, es = 4;
+    // ns: digit planes (3: the six products of weight >= 2^-26; 2: the three of
+    // weight >= 2^-19, BK_F32_I8X2); tj: the output tile's columns (128 / 256)
+    int npad = 0, R = 0, T128 = 0, T64 = 0, es = 4, ns = 3, tj = 128;
     int64_t dp = 0, plane = 0, ntile64 = 0;
     std::vector<int64_t> rb;  // range boundaries (R + 1, multiples of 64 columns)
     std::vector<int> order;   // per workgroup {tile I | J << 16, range (-1: idle)}
 };
-I8Layout i8_layout(int n, int64_t d, int es, int num_cu);
+I8Layout i8_layout(int n, int64_t d, int es, int num_cu, int ns = 3);
 size_t i8_workspace(const I8Layout &L);
 hipError_t configure_i8_kernels();
 // tables: device copy of {rb (R + 1 int64), order (int pairs)}; ws:

@@ -310,13 +310,15 @@ class Engine:
         _lib.BK_F32_MFMA (the fp32 MFMA, fp32 accumulation per K1 segment),
         _lib.BK_F32_CERTIFIED (the fp32 MFMA, re-run exactly on a near tie),
         _lib.BK_F32_I8 / _lib.BK_F32_I8_CERTIFIED (the Gram from exact int8
-        digit slices, K1i8)."""
+        digit slices, K1i8: three digits, six products), _lib.BK_F32_I8X2 /
+        _lib.BK_F32_I8X2_CERTIFIED (two digits, three products)."""
         check(lib().bk_set_f32_mode(self._ctx, int(mode)))
 
     def set_f64_mode(self, mode):
         """fp64 rows: BK_F64_EXACT (the fp64 MFMA), BK_F64_I8 (the Gram from exact
         int8 digit slices, error bound in the margin) or BK_F64_I8_CERTIFIED
-        (exact re-run on a near tie)."""
+        (exact re-run on a near tie); BK_F64_I8X2 / BK_F64_I8X2_CERTIFIED the
+        two-digit slicing."""
         check(lib().bk_set_f64_mode(self._ctx, int(mode)))
 
     def graph_enable(self, on=True):

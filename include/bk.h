@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 10
+#define BK_ABI_VERSION 11
 
 typedef struct bk_ctx bk_ctx;
 
@@ -139,7 +139,9 @@ enum bk_f32_mode {
     BK_F32_MFMA = 1,
     BK_F32_CERTIFIED = 2,
     BK_F32_I8 = 3,
-    BK_F32_I8_CERTIFIED = 4
+    BK_F32_I8_CERTIFIED = 4,
+    BK_F32_I8X2 = 5,
+    BK_F32_I8X2_CERTIFIED = 6
 };
 /* BK_F32_I8: the Gram from exact int8 digit slices on v_mfma_i32_32x32x32_i8
  * (bk_i8.hip, K1i8; the Ozaki scheme).  Per range of columns (at least 8,
@@ -156,6 +158,13 @@ enum bk_f32_mode {
  * max |x_i|^2) and several times faster.  Rows must be 16-B aligned (ld % 4 ==
  * 0, aligned base) and d >= 64; other batches take the exact path.  A
  * non-finite input makes the bound +inf (a near tie). */
+/* BK_F32_I8X2: the same slicing with TWO digits (x / s = a0/64 + a1/2^13 +
+ * rho, |rho| <= 2^-14) and the three digit products of weight >= 2^-19 (A0
+ * A0^T, A0 A1^T, A1 A0^T) on 128 x 256 output tiles: half the products and
+ * two thirds of the digit bytes of BK_F32_I8, under the absolute bound
+ *     sum_r 2^-14 (2 S_r L1_r + 1.0001 d_r S_r^2)
+ * (~2^7 looser than BK_F32_I8's; config E: still ~20x below its boundary
+ * gap).  BK_F32_I8X2_CERTIFIED re-runs a near tie exact. */
 /* BK_F32_CERTIFIED: the fp32 MFMA, then -- only when the selection margin
  * (bk_selection_margin) does not clear the fp32 bound -- the exact path on the
  * same device-resident batch, whose outputs replace the first run's.  Never
@@ -173,7 +182,13 @@ int bk_set_f32_mode(bk_ctx *ctx, int mode);
  * BK_F64_I8_CERTIFIED re-runs the fp64 MFMA on a near tie, so its selected
  * set is always the reference's.  The mean is unchanged (K4 reads the fp64
  * rows).  Rows must be 16-B aligned (even ld) and d >= 64. */
-enum bk_f64_mode { BK_F64_EXACT = 0, BK_F64_I8 = 3, BK_F64_I8_CERTIFIED = 4 };
+enum bk_f64_mode {
+    BK_F64_EXACT = 0,
+    BK_F64_I8 = 3,
+    BK_F64_I8_CERTIFIED = 4,
+    BK_F64_I8X2 = 5,          /* the two-digit slicing of BK_F32_I8X2 on fp64 rows */
+    BK_F64_I8X2_CERTIFIED = 6
+};
 int bk_set_f64_mode(bk_ctx *ctx, int mode);
 /* BK_F32_I8_CERTIFIED: the same contract on the int8-sliced Gram.
  * exact re-runs BK_F32_CERTIFIED / BK_F32_I8_CERTIFIED have made on this context */

@@ -14,11 +14,12 @@ ML/code/logistic_validator.py:54-65 on the same batch):
 
 * D_512x1M_f153, fp64, on the exact fp64 MFMA and on K1i8 (fp64 rows);
 * E_4096x262144_fp32 on the exact path (fp32 widened onto the fp64 MFMA), the
-  fp32 MFMA and K1i8.
+  fp32 MFMA and K1i8 (three and two digits; D too).
 
 The selection must equal the golden (these batches' boundary gaps clear every
-mode's bound: near_tie is False) and every shard's mean must be within the
-§8(d) bound.  The summed record carries the whole batch: its column count is
+mode's bound: near_tie is False; only D on the two-digit Gram may be flagged,
+and then the certified mode re-runs it exact) and every shard's mean must be
+within the §8(d) bound.  The summed record carries the whole batch: its column count is
 d, its fp32-MFMA column count is d on the fp32 MFMA path, and on K1i8 its
 Gram bound e_G is the rank-order sum of the eight shards' bounds, bit for bit.
 """
@@ -48,17 +49,18 @@ def _batch(engine, name):
 
 def _set_mode(engine, dt, mode):
     if dt == _lib.BK_F64:
-        engine.set_f64_mode({"exact": _lib.BK_F64_EXACT, "i8": _lib.BK_F64_I8}[mode])
+        engine.set_f64_mode({"exact": _lib.BK_F64_EXACT, "i8": _lib.BK_F64_I8,
+                             "i8x2": _lib.BK_F64_I8X2}[mode])
         engine.set_f32_mode(_lib.BK_F32_EXACT)
     else:
         engine.set_f32_mode({"exact": _lib.BK_F32_EXACT, "mfma": _lib.BK_F32_MFMA,
-                             "i8": _lib.BK_F32_I8}[mode])
+                             "i8": _lib.BK_F32_I8, "i8x2": _lib.BK_F32_I8X2}[mode])
         engine.set_f64_mode(_lib.BK_F64_EXACT)
 
 
-CASES = [("D_512x1M_f153", "exact"), ("D_512x1M_f153", "i8"),
+CASES = [("D_512x1M_f153", "exact"), ("D_512x1M_f153", "i8"), ("D_512x1M_f153", "i8x2"),
          ("E_4096x262144_fp32", "exact"), ("E_4096x262144_fp32", "mfma"),
-         ("E_4096x262144_fp32", "i8")]
+         ("E_4096x262144_fp32", "i8"), ("E_4096x262144_fp32", "i8x2")]
 
 
 @pytest.mark.parametrize("name,mode", [c for c in CASES if GU.have(c[0])])
@@ -104,7 +106,7 @@ def test_eight_shard_records_finish_like_the_golden(engine, name, mode):
     for r in recs:
         eg += float(r[2])
     assert tail[2] == eg
-    if mode == "i8":
+    if mode in ("i8", "i8x2"):
         assert all(r[2] > 0 for r in recs)
     else:
         assert eg == 0.0
@@ -115,8 +117,14 @@ def test_eight_shard_records_finish_like_the_golden(engine, name, mode):
     assert mg["d"] == d and all(m == mg for m in margins)
     print("%s %s x%d: gap %.4g err_bound %.4g near_tie %s e_G %.4g"
           % (name, mode, SHARDS, mg["gap"], mg["err_bound"], mg["near_tie"], eg))
-    assert not mg["near_tie"], mg
-    assert np.array_equal(sels[0], g["sel"])
+    if mg["near_tie"]:
+        # only an approximate Gram may leave the boundary within its bound (the
+        # certified modes then re-run exact); the exact sums never do here
+        assert mode in ("mfma", "i8", "i8x2") and not mg["gap"] > mg["err_bound"], mg
+    else:
+        assert np.array_equal(sels[0], g["sel"])
+    if mode in ("exact", "i8") or name.startswith("E_"):
+        assert not mg["near_tie"], mg  # these gaps clear the bound
     scores = sc.cpu().numpy()
     err = float(np.max(np.abs(scores - g["scores"])))
     assert err <= mg["err_bound"] / 2 + 1e-9 * float(np.max(np.abs(g["scores"])))
