@@ -608,8 +608,9 @@ __global__ __launch_bounds__(RB_NT) void k_roni_batch(const float *__restrict__ 
                                                       const int64_t *__restrict__ idx, int64_t nb,
                                                       double g, double *__restrict__ scores,
                                                       int32_t *__restrict__ near_out) {
-    __shared__ float xs[2][RB_ST][RB_KP];
-    __shared__ float wsm[2][16][RB_KP];
+    // read through 16-B (f4) casts: aligned explicitly, not by the LDS layout's luck
+    __shared__ __attribute__((aligned(16))) float xs[2][RB_ST][RB_KP];
+    __shared__ __attribute__((aligned(16))) float wsm[2][16][RB_KP];
     __shared__ float lgs[2][RB_ST][16];
     __shared__ double xnl[2][RB_ST], wnl[2][16], bl[2][16];
     __shared__ int64_t srow[2][RB_ST];

@@ -83,7 +83,11 @@ class SoftmaxRONIValidator(RONIValidator):
     scores every evaluation over the whole set (bk_roni_softmax).
 
     After each call, last_near_ties holds the per-evaluation near-tie counts
-    (bk.h: where torch's fp32 argmax may differ from this one)."""
+    (bk.h: where torch's fp32 argmax may differ from this one) and last_idx
+    the (n, 2, nb) sample indices it scored (None for whole-set scores): the
+    reference's scores are random draws (client.py:136-144), so a decision is
+    reproduced by passing last_idx back as idx, or by a fixed seed.  A
+    validator built with seed=None draws from fresh OS entropy each run."""
 
     def __init__(self, Xvalid, yvalid, n_classes, engine: Optional[Engine] = None,
                  priv_prob: float = 0.0, batch_size: Optional[int] = 10, seed=None):
@@ -101,6 +105,7 @@ class SoftmaxRONIValidator(RONIValidator):
             raise ValueError("batch_size must be >= 1")
         self._rng = np.random.default_rng(seed)
         self.last_near_ties = None
+        self.last_idx = None
         check(lib().bk_roni_softmax_set_validation(self._engine.ctx, X.ctypes.data, self.nv,
                                                    self.d_in, self.d_in, y.ctypes.data,
                                                    self.n_classes))
@@ -128,8 +133,10 @@ class SoftmaxRONIValidator(RONIValidator):
             check(lib().bk_roni_softmax(self._engine.ctx, ww.ctypes.data, D.ctypes.data, n,
                                         self.d, out.ctypes.data, nt.ctypes.data))
             self.last_near_ties = nt
+            self.last_idx = None
             return out
         idx = self.draw_batches(n) if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        self.last_idx = idx
         if idx.ndim != 3 or idx.shape[:2] != (n, 2):
             raise ValueError("idx must be (n, 2, nb)")
         nt = np.empty((n, 2), dtype=np.int32)
