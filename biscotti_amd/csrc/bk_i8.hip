@@ -82,6 +82,27 @@ constexpr int64_t I8_CHUNK_STRIDE = BK_I8_BLOCKED ? 8192 : I8_KC;
 #define BK_I8_MAP 1
 #endif
 constexpr int I8_LDS = 2 * I8_STAGE;               // 96 KiB: two stages
+#ifndef BK_I8_ABL
+#define BK_I8_ABL 0
+#endif
+// waves per workgroup of the two- and three-digit Gram kernels (4: one per
+// SIMD, 64 x 128 / 64 x 64 per wave; 8: two per SIMD, 64 x 64 / 64 x 32)
+#ifndef BK_I8_W2
+#define BK_I8_W2 4
+#endif
+#ifndef BK_I8_W3
+#define BK_I8_W3 4
+#endif
+constexpr int I8_NBJ2 = BK_I8_W2 == 8 ? 2 : 4, I8_NBJ3 = BK_I8_W3 == 8 ? 1 : 2;
+// the super-block of the tile order (i8_layout): BK_I8_SBI row blocks of 128
+// by BK_I8_SBC columns (in units of 128) -- an XCD's ~32 concurrent tiles
+// share these row blocks in its L2
+#ifndef BK_I8_SBI
+#define BK_I8_SBI 4
+#endif
+#ifndef BK_I8_SBC
+#define BK_I8_SBC 4
+#endif
 constexpr int I8_RANGE_BYTES = 131072;             // a row's slice of one column range (i8_layout)
 // the exponent of a (row, range) slice holding a NaN or an infinity: its
 // digits are zero, k_gram_i8 writes NaN into every Gram element of that row
@@ -290,19 +311,27 @@ __device__ __forceinline__ int i8_swz(int row, int g) { return g ^ ((row >> 2) &
 // 24 MFMAs against 12 fragment reads per 32-column k-step and wave, so the
 // two-digit tile does the same instruction stream per chunk for twice the
 // output elements and half the products each.
-template <int NS, int NBJ>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// NW: waves per workgroup, 4 (one per SIMD) or 8 (two per SIMD: while one
+// wave waits on its LDS fragment reads or the barrier, the other issues
+// MFMAs); the waves tile the output 2 x NW/2, each 64 x 32 NBJ.
+template <int NS, int NBJ, int NW = 4>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4)))
 void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                const int64_t *__restrict__ rb, int R, const int2 *__restrict__ order,
                const int *__restrict__ es, int n, int T64, double *__restrict__ part,
                int64_t ntile64) {
-    constexpr int TJ = 64 * NBJ;                       // the tile's columns (rows of operand B)
+    constexpr int NT = 64 * NW;                        // threads
+    constexpr int TJ = (NW / 2) * 32 * NBJ;            // the tile's columns (rows of operand B)
+    constexpr int NGR = I8_STAGE / 16 / NT;            // 16-B granules each thread stages per chunk
+    constexpr int NMF = (NS == 3 ? 6 : 3) * 2 * NBJ;   // MFMAs per k-step and wave
+    constexpr int NRD = NS * (2 + NBJ);                // fragment reads per k-step and wave
     constexpr int NL = NS;                             // accumulator levels
     constexpr int NP = NS == 3 ? 6 : 3;                // digit products
     constexpr int A_BYTES = NS * I8_TILE * I8_KC;      // operand A (the tile's rows) per stage
     constexpr int B_PLANE = TJ * I8_KC;
     static_assert(A_BYTES + NS * B_PLANE == I8_STAGE, "48 KiB stages");
-    static_assert(NP * 2 * NBJ == 24 && NS * (2 + NBJ) == 12, "24 MFMAs per 12 reads");
+    static_assert(NW == 4 ? (NMF == 24 && NRD == 12 && NGR == 12) : (NW == 8 && NGR == 6),
+                  "4 waves: 24 MFMAs per 12 reads, 12 granules; 8 waves: 6 granules");
     extern __shared__ __attribute__((aligned(16))) int8_t lds[];  // two stages of I8_STAGE bytes
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -314,14 +343,14 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
     const int r = item.y, I = item.x & 0xffff, J = item.x >> 16;
     const int64_t k0 = rb[r], k1 = rb[r + 1];
     const int nch = (int)((k1 - k0) / I8_KC);
-    // staging: granule q = tid + 256 u (u < 12) of the chunk: q < 512 NS is
+    // staging: granule q = tid + NT u (u < NGR) of the chunk: q < 512 NS is
     // operand A (digit q >> 9, row (q >> 2) & 127), the rest operand B (digit
     // q' / (4 TJ), row (q' >> 2) % TJ); g = q & 3 the 16-B granule of the row
-    const int8_t *src[12];
-    int dst[12];
+    const int8_t *src[NGR];
+    int dst[NGR];
 #pragma unroll
-    for (int u = 0; u < 12; ++u) {
-        const int q = tid + 256 * u;
+    for (int u = 0; u < NGR; ++u) {
+        const int q = tid + NT * u;
         const int g = q & 3;
         int t, row, grow, off;
         if (q < 512 * NS) {
@@ -339,14 +368,22 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
         src[u] = S + (int64_t)t * plane + i8_off(grow, k0 + 16 * g, dp);
         dst[u] = off + row * I8_KC + 16 * i8_swz(row, g);
     }
-    v4i pf[12];
+    v4i pf[NGR];
+    // BK_I8_ABL (timing-only ablations, tools/ builds; the product is 0): 1 =
+    // every chunk fetch from the range's first 4 chunks (L2-resident: no HBM /
+    // Infinity Cache latency), 2 = no LDS stores, 3 = no fragment reads, 4 = no MFMAs
     auto fetch = [&](int ch) {
+        if constexpr (BK_I8_ABL == 1) ch &= 3;
 #pragma unroll
-        for (int u = 0; u < 12; ++u) pf[u] = *reinterpret_cast<const v4i *>(src[u] + (int64_t)ch * I8_CHUNK_STRIDE);
+        for (int u = 0; u < NGR; ++u) pf[u] = *reinterpret_cast<const v4i *>(src[u] + (int64_t)ch * I8_CHUNK_STRIDE);
     };
     auto put = [&](int8_t *b) {
+        if constexpr (BK_I8_ABL == 2) {
+            if (nch > 1000000) b[dst[0]] = (int8_t)pf[0][0];  // keep the loads
+            return;
+        }
 #pragma unroll
-        for (int u = 0; u < 12; ++u) *reinterpret_cast<v4i *>(b + dst[u]) = pf[u];
+        for (int u = 0; u < NGR; ++u) *reinterpret_cast<v4i *>(b + dst[u]) = pf[u];
     };
     v16i acc[NL][2][NBJ];
 #pragma unroll
@@ -355,10 +392,14 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
         for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < NBJ; ++b) acc[l][a][b] = v16i{};
-    const int wr = (wave & 1) * 64, wc = (wave >> 1) * (32 * NBJ);
+    const int wr = (wave & 1) * 64, wc = (wave >> 1) * (32 * NBJ);  // this wave's 64 x 32 NBJ
     const int fr = lane & 31, fh = lane >> 5;
     // the fragments of k-step ks (32 columns: granules 2 ks + fh) of stage b
     auto frags = [&](const int8_t *b, int ks, v4i (&fa)[NS][2], v4i (&fb)[NS][NBJ]) {
+        if constexpr (BK_I8_ABL == 3) {
+            if (ks == 0 && b == nullptr) fa[0][0] = v4i{1, 1, 1, 1};  // (never) the registers as they are
+            return;
+        }
         const int g = 2 * ks + fh;
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
@@ -380,6 +421,10 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
     // over the blocks: consecutive MFMAs never accumulate into the same
     // registers.  (Measured neutral against block-major chains at config E.)
     auto mma = [&](const v4i (&fa)[NS][2], const v4i (&fb)[NS][NBJ]) {
+        if constexpr (BK_I8_ABL == 4) {
+            acc[0][0][0][0] += fa[0][0][0] ^ fb[0][0][1];  // keep the reads
+            return;
+        }
         constexpr int PT[6][3] = {{0, 0, 0}, {1, 0, 1}, {1, 1, 0}, {2, 0, 2}, {2, 1, 1}, {2, 2, 0}};
 #pragma unroll
         for (int p = 0; p < NP; ++p)
@@ -417,11 +462,19 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
         auto body = [&](int ch, int8_t *__restrict__ C, const int8_t *__restrict__ N) {
             mma(F0a, F0b);
             frags(C, 1, F1a, F1b);
+            if constexpr (NW == 4) {
 #pragma unroll
-            for (int q = 0; q < 12; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                for (int q = 0; q < 12; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                }
+            } else {  // the reads first (the other wave of the SIMD covers their latency)
+#pragma unroll
+                for (int q = 0; q < NMF; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (q < NRD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);  // no motion across the phases
             __syncthreads();
@@ -429,13 +482,23 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
             frags(N, 0, F0a, F0b);
             put(C);
             fetch(cl(ch + 3));
+            if constexpr (NW == 4) {
 #pragma unroll
-            for (int q = 0; q < 12; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+                for (int q = 0; q < 12; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                    __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < NMF; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (q < NGR) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    if (q < NRD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    if (q < NGR) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         };
@@ -480,11 +543,21 @@ __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ pa
                                                    const double *__restrict__ bound) {
     const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
     if (e < usz) {
+        // ranges in order, 8 loads in flight per thread (R is a multiple of 8)
         d2v acc = *reinterpret_cast<const d2v *>(part + e);
-        for (int r = 1; r < R; ++r) {
-            const d2v v = *reinterpret_cast<const d2v *>(part + (int64_t)r * usz + e);
-            acc.x += v.x;
-            acc.y += v.y;
+        for (int r0 = 1; r0 < R; r0 += 8) {
+            d2v v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                v[u] = r0 + u < R ? __builtin_nontemporal_load(reinterpret_cast<const d2v *>(
+                                        part + (int64_t)(r0 + u) * usz + e))
+                                  : d2v{0.0, 0.0};
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (r0 + u < R) {
+                    acc.x += v[u].x;
+                    acc.y += v[u].y;
+                }
         }
         *reinterpret_cast<d2v *>(U + e) = acc;
     }
@@ -520,7 +593,7 @@ I8Layout i8_layout(int n, int64_t d, int es, int num_cu, int ns) {
     // no tile past the last row; super-blocked (4 row blocks x 512 columns,
     // row by row) so consecutive tiles share row blocks
     const int TI = (n + I8_TILE - 1) / I8_TILE, TJn = (n + L.tj - 1) / L.tj, rj = L.tj / I8_TILE;
-    const int SBI = 4, SBJ = 4 / rj;
+    const int SBI = BK_I8_SBI, SBJ = BK_I8_SBC / rj > 0 ? BK_I8_SBC / rj : 1;
     std::vector<int> tiles;  // I | J << 16
     for (int BI = 0; BI < (TI + SBI - 1) / SBI; ++BI)
         for (int BJ = 0; BJ < (TJn + SBJ - 1) / SBJ; ++BJ)
@@ -596,10 +669,10 @@ size_t i8_workspace(const I8Layout &L) {
 }
 
 hipError_t configure_i8_kernels() {
-    hipError_t e = hipFuncSetAttribute((const void *)k_gram_i8<3, 2>,
+    hipError_t e = hipFuncSetAttribute((const void *)k_gram_i8<3, I8_NBJ3, BK_I8_W3>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, I8_LDS);
     if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void *)k_gram_i8<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    return hipFuncSetAttribute((const void *)k_gram_i8<2, I8_NBJ2, BK_I8_W2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                I8_LDS);
 }
 
@@ -668,10 +741,10 @@ hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables
     const int2 *order = (const int2 *)((const char *)tables + (size_t)(L.R + 1) * 8);
     const int64_t items = (int64_t)L.order.size() / 2;  // one workgroup each
     if (L.ns == 2)
-        hipLaunchKernelGGL((k_gram_i8<2, 4>), dim3((unsigned)items), dim3(256), I8_LDS, st, w.S, L.dp,
+        hipLaunchKernelGGL((k_gram_i8<2, I8_NBJ2, BK_I8_W2>), dim3((unsigned)items), dim3(64 * BK_I8_W2), I8_LDS, st, w.S, L.dp,
                            L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
     else
-        hipLaunchKernelGGL((k_gram_i8<3, 2>), dim3((unsigned)items), dim3(256), I8_LDS, st, w.S, L.dp,
+        hipLaunchKernelGGL((k_gram_i8<3, I8_NBJ3, BK_I8_W3>), dim3((unsigned)items), dim3(64 * BK_I8_W3), I8_LDS, st, w.S, L.dp,
                            L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
     return hipGetLastError();
 }

@@ -61,8 +61,9 @@ def main():
     lib0, ctx0 = builds[0][1], builds[0][2]
     lib0.bk_synth_fill_device(ctx0, X.data_ptr(), dt, n, d, d, 0, d, 1, n // 3, 0.01, 0.05, 1e-3, 0)
     lib0.bk_synchronize(ctx0)
+    mode = int(os.environ.get("MODE", 3))  # 3: three digits (BK_F32_I8); 5: two (BK_F32_I8X2)
     for label, lib, ctx, env in builds:
-        st = (lib.bk_set_f64_mode(ctx, 3) if f64 else lib.bk_set_f32_mode(ctx, 3))
+        st = (lib.bk_set_f64_mode(ctx, mode) if f64 else lib.bk_set_f32_mode(ctx, mode))
         assert st == 0, lib.bk_last_error()
     ue = int(lib0.bk_upper_elems(n))
     Us = {b[0]: torch.empty(ue, dtype=torch.float64, device="cuda") for b in builds}
@@ -72,7 +73,7 @@ def main():
             res[label].append(run(lib, ctx, X.data_ptr(), dt, n, d, Us[label].data_ptr(), reps))
     torch.cuda.synchronize()
     ref = Us[builds[0][0]]
-    ops = 6 * n * (n + 1) * d
+    ops = (3 if mode == 5 else 6) * n * (n + 1) * d
     for label, v in res.items():
         med = {k: sorted(x[k] for x in v)[len(v) // 2] for k in KIDS}
         same = bool(torch.equal(Us[label], ref))
