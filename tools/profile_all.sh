@@ -5,7 +5,7 @@
 # host with tools/pmc_summary.py (it stamps the libbk.so hash bench.py checks):
 #   tools/profile_all.sh                      (on the GPU box, via gpurun)
 #   then here, per tag: python tools/pmc_summary.py gpurun_out/prof_<tag> <tag> \
-#       profiles/r04/rocprof_<tag>_r04 <warmup> <steps>   (10 40; E: 5 10)
+#       profiles/r05/rocprof_<tag>_r05 <warmup> <steps>   (10 40; E: 5 10)
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 run() {
@@ -15,8 +15,9 @@ run() {
 }
 run D_512x1M_f153
 run D_512x1M_f153_i8_certified --f32-mode i8_certified
+run D_512x1M_f153_i8x2_certified --f32-mode i8x2_certified
 run C_1024x131072 --workload C_1024x131072
-for m in exact mfma certified i8 i8_certified; do
+for m in exact mfma certified i8 i8_certified i8x2 i8x2_certified; do
   t=E_4096x262144_fp32; [ "$m" = exact ] || t="${t}_$m"
   run "$t" --workload E_4096x262144_fp32 --f32-mode "$m" --steps 10 --warmup 5
 done
