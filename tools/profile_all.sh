@@ -3,13 +3,20 @@
 # tools/profile.sh run (kernel trace + stats of bench.py, then one --pmc pass
 # per counter group) per config.  Summaries are made afterwards on the build
 # host with tools/pmc_summary.py (it stamps the libbk.so hash bench.py checks):
-#   tools/profile_all.sh                      (on the GPU box, via gpurun)
+#   tools/profile_all.sh [tag patterns...]    (on the GPU box, via gpurun; e.g. 'E_*')
 #   then here, per tag: python tools/pmc_summary.py gpurun_out/prof_<tag> <tag> \
 #       profiles/r05/rocprof_<tag>_r05 <warmup> <steps>   (10 40; E: 5 10)
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
+# optional arguments: only the tags matching one of these shell patterns
+ONLY=("$@")
 run() {
   tag=$1; shift
+  if [ ${#ONLY[@]} -gt 0 ]; then
+    hit=0
+    for p in "${ONLY[@]}"; do case "$tag" in $p) hit=1 ;; esac; done
+    [ $hit = 1 ] || return 0
+  fi
   echo "=== profile $tag: $*"
   "$R/tools/profile.sh" "$tag" "$@" || { echo "profile $tag failed rc=$?"; exit 1; }
 }
