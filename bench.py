@@ -837,7 +837,13 @@ def launch_ranks(a, argv=None, gpus_fn=visible_gpus):
            "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
     log("bench.py: launching %d ranks: %s" % (a.gpus, " ".join(cmd)))
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import signal
     p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, text=True)
+
+    def forward(sig, _frame):  # a time limit that signals this parent reaches the ranks too
+        p.send_signal(sig)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
     lines = []
     for ln in p.stdout:  # rank 0's line (the ranks send everything else to stderr)
         if ln.strip():

@@ -71,3 +71,18 @@ def test_launcher_refuses_fewer_gpus_than_rccl_ranks():
     assert bench.launch_ranks(a, argv=["--gpus", "8"], gpus_fn=lambda: 1) != 0
     a = argparse.Namespace(gpus=2, exchange="host")
     assert bench.launch_ranks(a, argv=["--gpus", "2"], gpus_fn=lambda: 0) != 0
+
+
+def test_launcher_relays_the_ranks_failure(capfd):
+    """The launcher's child torch.distributed.run: here (no GPU) the ranks
+    fail, and the parent must return their non-zero status with nothing on
+    stdout -- never a 1-GPU line in place of the N-rank one."""
+    import argparse
+    sys.path.insert(0, REPO)
+    import bench
+    a = argparse.Namespace(gpus=2, exchange="host")
+    rc = bench.launch_ranks(a, argv=["--gpus", "2", "--exchange", "host", "--steps", "1",
+                                     "--warmup", "0", "--workload", "A_creditcard",
+                                     "--no-cpu-baseline"], gpus_fn=lambda: 1)
+    out = capfd.readouterr().out
+    assert rc != 0 and not out.strip()
