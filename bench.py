@@ -178,8 +178,8 @@ I8_PRODUCTS = {"i8": 6, "i8_certified": 6,  # K1i8's digit products (bk_i8.hip):
 def gram_roofline(n, dl, k_ms, dtype, f32_mode, exact_rerun=False):
     """The dominant kernel's roofline for the arithmetic it ran: fp64 MFMA
     (fp64 rows, fp32 rows exact), fp32 MFMA (BK_F32_MFMA / CERTIFIED), int8
-    MFMA (BK_F32_I8*: 6 digit products per Gram element; achieved in int8
-    TOPS, plus the fp64-equivalent rate n(n+1) d / t)."""
+    MFMA (BK_F32_I8*: 6 digit products per Gram element, BK_F32_I8X2*: 3;
+    achieved in int8 TOPS, plus the fp64-equivalent rate n(n+1) d / t)."""
     flops = n * (n + 1) * dl
     i8 = f32_mode in I8_MODE_NAMES  # fp32 rows (BK_F32_I8*) or fp64 rows (BK_F64_I8*)
     mode = "exact" if exact_rerun or (dtype != "f32" and not i8) else f32_mode
