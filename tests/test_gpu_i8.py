@@ -434,3 +434,30 @@ def test_i8_workspace_failure_runs_exact(oracle, monkeypatch):
         assert np.array_equal(sel, oracle.krum(X, 90)[0])
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("mode", I8_MODES, ids=MODE_IDS.get)
+def test_i8_at_max_n(engine, oracle, mode):
+    """BK_MAX_N = 16,384 rows on K1i8 (128 row blocks; two digits: 64 column
+    blocks of 256, rows padded to 256): the Gram of digit-representable rows
+    equals the exact one bit for bit, and Multi-Krum on them selects the
+    oracle's set."""
+    from biscotti_amd.dist import unpack_upper
+    n, d, f = 16384, 192, 4915
+    rng = np.random.default_rng(16384)
+    X = rng.integers(-63, 64, size=(n, d)).astype(np.float32)
+    X *= (2.0 ** rng.integers(-6, 7, size=(n, 1))).astype(np.float32)
+    want = _upper(engine, X, _lib.BK_F32_EXACT)
+    got = _upper(engine, X, mode)
+    assert got[-2] == pytest.approx(_bound(X, NS_OF[mode]), rel=1e-12)
+    Gw, Gg = unpack_upper(want, n), unpack_upper(got, n)
+    assert np.array_equal(Gg, Gw)
+    del Gw, Gg
+    engine.set_f32_mode(mode)
+    try:
+        sel, _, _ = engine.multikrum(X, f)
+        mg = engine.selection_margin()
+    finally:
+        engine.set_f32_mode(_lib.BK_F32_EXACT)
+    osel, _, _ = oracle.krum(X, f)
+    assert np.array_equal(sel, osel) or mg["near_tie"]
