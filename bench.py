@@ -306,6 +306,111 @@ def device_variant(eng, dev, name, f32_mode="exact", steps=20, warmup=5, X=None)
     return out
 
 
+# config E in its multi-GPU form (BASELINE configs[4]: fp32, 8 x MI355X): the
+# exact path, the fp32 MFMA the config names, and the certified two-digit int8 Gram
+E_SHARD_MODES = ("exact", "mfma", "i8x2_certified")
+
+
+def sharded_variant(eng, dev, name, f32_mode, nparts, rank, world, barrier, emu, steps=10,
+                    warmup=5):
+    """A BASELINE config in its d-sharded multi-GPU form: this
+    rank's column shard through libbk's sharded entry (K1 on the shard, the
+    RCCL all-reduce of the packed Gram, split scoring at n >= 2049, the local
+    mean).  Timed like the headline: warm-up, barrier, K steps, barrier, max
+    over ranks; K1 and the exchange evented live on libbk's stream.  With
+    emu > 1 (one GPU): rank 0's shard of an emu-rank job, its rate."""
+    import hashlib
+    import torch
+    import torch.distributed as tdist
+    from biscotti_amd import _lib
+    from biscotti_amd.dist import shard_bounds
+    w = WORKLOADS[name]
+    n, d, f = w["n"], w["d"], w["f"]
+    m = n - f
+    bdt = _lib.BK_F32 if w["dtype"] == "f32" else _lib.BK_F64
+    es = 4 if w["dtype"] == "f32" else 8
+    c0, dl = shard_bounds(d, nparts, rank)
+    X = torch.empty((n, max(dl, 1)), dtype=torch.float32 if es == 4 else torch.float64, device=dev)
+    eng.synth_fill_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), c0, d, w["seed"], w["nbyz"],
+                       flags=w.get("flags", 0))
+    sel = torch.empty(m, dtype=torch.int64, device=dev)
+    sc = torch.empty(n, dtype=torch.float64, device=dev)
+    mean = torch.empty(max(dl, 1), dtype=torch.float64, device=dev)
+
+    def step():
+        eng.multikrum_sharded_ptr(X.data_ptr(), bdt, n, dl, X.stride(0), f, sel.data_ptr(),
+                                  sc.data_ptr(), mean.data_ptr())
+
+    set_mode = eng.set_f64_mode if w["dtype"] == "f64" else eng.set_f32_mode
+    set_mode(F32_MODES[f32_mode])
+    try:
+        r0 = eng.certified_reruns()
+        for _ in range(max(5, warmup)):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        eng.timing_select(["k_gram", "allreduce", "score_gather"])
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kt = eng.timing_read()
+        eng.timing_select([])
+        eng.timing_enable(True)  # the per-kernel breakdown, an untimed pass
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        kb = eng.timing_read()
+        eng.timing_enable(False)
+        mg = eng.selection_margin()
+        reruns = eng.certified_reruns() - r0
+    finally:
+        set_mode(0)
+    if world > 1:
+        el = max_over_ranks(el, dev)
+    ms = el / steps * 1e3
+    k1 = kt.get("k_gram", {"avg_ms": float("nan")})["avg_ms"]
+    roof = gram_roofline(n, dl, k1, w["dtype"], f32_mode, exact_rerun=reruns > 0)
+    h = hashlib.sha256(sel.cpu().numpy().tobytes()).hexdigest()[:16]
+    hs = [h]
+    def avg(kid):
+        v = kt.get(kid)
+        return round(v["avg_ms"], 4) if v else None
+    mine = {"rank": rank, "k_gram_ms": round(k1, 4), "exchange_ms": avg("allreduce"),
+            "score_gather_ms": avg("score_gather")}
+    per_rank = [mine]
+    if world > 1:
+        hs, per_rank = [None] * world, [None] * world
+        tdist.all_gather_object(hs, h)
+        tdist.all_gather_object(per_rank, mine)
+    if emu:
+        par = {"n/a": "emulated rank 0 of %d: 1/%d of the columns" % (emu, emu)}
+    else:
+        par = golden_check(name, sel.cpu().numpy(), mean[:dl].cpu().numpy(), c0, dl) or {}
+        par["margin"] = {"near_tie": mg["near_tie"], "gap": mg["gap"], "err_bound": mg["err_bound"]}
+    out = {"n": n, "d": d, "f": f, "m": m, "dtype": w["dtype"], "f32_mode": f32_mode,
+           "parallelism": ("emulated rank 0 of %d (1 GPU)" % emu if emu else
+                           "d-shard x%d + RCCL all-reduce" % world),
+           "d_local": dl, "warmup": max(5, warmup), "steps": steps, "ms_per_step": round(ms, 4),
+           "value": round(n * (dl if emu else d) * es / (ms * 1e-3) / 1e9, 3), "unit": "GB/s",
+           "roofline": dict(roof, kernel="k_gram", kernel_avg_ms=round(k1, 4)),
+           "kernels_ms_avg": {k: round(v["avg_ms"], 5) for k, v in kb.items()},
+           "exchange_ms": max((p["exchange_ms"] for p in per_rank if p["exchange_ms"] is not None),
+                              default=None),
+           "score_gather_ms": max((p["score_gather_ms"] for p in per_rank
+                                   if p["score_gather_ms"] is not None), default=None),
+           "per_rank": per_rank, "ranks_agree": len(set(hs)) == 1, "parity": par}
+    if f32_mode.endswith("certified"):
+        out["certified_reruns"] = reruns
+    del X
+    torch.cuda.empty_cache()
+    return out
+
+
 def host_entry_variant(eng, dev, name, steps=200, warmup=20, single_calls=7, idle_s=0.2):
     """What a Biscotti verifier's own call costs (krum.go:100-166: the batch
     arrives over RPC into host slices): bk_multikrum(BK_HOST_PINNED) from a
@@ -717,6 +822,9 @@ def _summ(v, host=None):
          "near_tie": (par.get("margin") or {}).get("near_tie")}
     if "certified_reruns" in v:
         s["reruns"] = v["certified_reruns"]
+    if "per_rank" in v:  # a d-sharded variant: the slowest rank's exchange and score gather
+        s["exchange_ms"] = v.get("exchange_ms")
+        s["score_gather_ms"] = v.get("score_gather_ms")
     if host:
         s["host_ms"] = host.get("ms_per_call")
         s["host_over_h2d_ms"] = host.get("overhead_over_h2d_ms")
@@ -945,6 +1053,10 @@ def main():
     bdt = _lib.BK_F32 if w["dtype"] == "f32" else _lib.BK_F64
     es = 4 if w["dtype"] == "f32" else 8
 
+    if emu:
+        # split scoring as rank 0 of emu ranks would run it (n >= 2049: config
+        # E): its share of K2's rows only, once a mode's first call scored all
+        os.environ["BK_EMU_SPLIT_SCORES"] = str(emu)
     eng = Engine(dev_idx)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     # fp64 rows take the int8 modes through bk_set_f64_mode (K1i8 for fp64 rows)
@@ -1104,6 +1216,13 @@ def main():
                              **({"traffic_ratio_to_unique_bytes": round(tr2 / (n * dl * es), 3)}
                                 if tr2 else {})),
             "parity": par2}
+
+    if sharded and not host_exch and not a.no_variants and a.workload == DEFAULT_WORKLOAD:
+        # config E at this rank count (BASELINE: fp32, 8 x MI355X), each rank
+        # its own column shard, beside the headline D (d-sharded the same way)
+        for mode in E_SHARD_MODES:
+            variants[workload_tag("E_4096x262144_fp32", mode)] = sharded_variant(
+                eng, dev, "E_4096x262144_fp32", mode, emu or world, rank, world, barrier, emu)
 
     # roofline of the dominant kernel (K1, fp64 MFMA): algorithmic flops per
     # launch = n(n+1) * d_local (symmetric Gram incl. diagonal)

@@ -61,7 +61,7 @@ const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_transpo
                                             "k_rank",    "k_compact", "k_mean",   "allreduce",
                                             "k_synth",   "h2d",       "d2h",
                                             "k_aggregate", "k_qsum",  "k_noise",
-                                            "k_roni", "k_small", "k_slice"};
+                                            "k_roni", "k_small", "k_slice", "score_gather"};
 
 struct DevBuf {
     void *p = nullptr;
@@ -184,6 +184,18 @@ struct bk_ctx {
     DevBuf status;
     int test_fail_exchange = 0;  // test knob BK_TEST_FAIL_BEFORE_EXCHANGE (bk_create)
     int test_i8_enomem = 0;      // test knob BK_TEST_I8_ENOMEM: K1i8's workspace "fails" (bk_create)
+    // split scoring (stage_finish): at n >= split_min_n each rank of a sharded
+    // call scores its share of the rows and the ranks all-gather the scores
+    // (BK_SPLIT_SCORES_MIN_N; 0 turns it off).  Knobs for a 1-rank
+    // communicator (bk_create): BK_TEST_SPLIT_SCORES=R scores in R row chunks,
+    // one launch each, as R ranks would (the arithmetic of the split, tested on
+    // one GPU); BK_EMU_SPLIT_SCORES=R scores only rank 0's chunk once a mode's
+    // first call has scored them all (bench.py --emulate-ranks: one rank's time)
+    int64_t split_min_n = 2049;
+    int test_split_scores = 0, emu_split_scores = 0;
+    int test_split_fail = 0;   // BK_TEST_SPLIT_FAIL=p: under BK_TEST_SPLIT_SCORES, share p - 1 "fails"
+    int64_t emu_split_n = -1;  // emulation: the n whose other chunks are scored
+    DevBuf sgather;            // the gathered scores: parts x chunk doubles
     int64_t exchanges = 0;        // exchanges of the packed Gram (bk_comm_stats)
     double exchanged_bytes = 0;   // bytes each rank put into them
 };
@@ -223,7 +235,7 @@ void bind_epoch(bk_ctx *c) {
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                       &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
                       &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws,
-                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws};
+                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws, &c->sgather};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -550,19 +562,68 @@ int margin_rec(bk_ctx *c) {
     return BK_OK;
 }
 
-// K2 + K3 + K4 from a packed upper Gram
-int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int dtype,
-                 int64_t n, int64_t d, int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
-                 double *d_mean) {
-    CHK(ensure(c->mask, (size_t)n * sizeof(int)));
-    double *sc = d_scores;
-    if (!sc) {
-        CHK(ensure(c->scores, (size_t)n * sizeof(double)));
-        sc = (double *)c->scores.p;
+// Split scoring over the ranks of a sharded call (after the
+// exchange every rank holds the whole Gram, and K2 -- n sorts of n distances,
+// 0.2 ms at n = 4,096 -- was repeated on every rank): rank r scores rows
+// [r ch, r ch + ch), ch = ceil(n / parts), into slice r of a parts x (ch + 1)
+// buffer whose last word is the rank's status (0, or NaN when its share
+// failed), and ONE in-place RCCL all-gather hands every rank all n scores.
+// Each row's score is K2's, bitwise, whichever rank computes it.
+// k_split_unpack then copies the scores to the caller's array and hands K3b
+// the Gram's trailing record, made NaN if any rank's status is not 0 -- so a
+// rank that failed its share marks the call invalid on every rank
+// (MARGIN_POISONED), as a shard that fails before the exchange does.  Only on
+// the transposed K2 path (n >= 2049), whose contiguous diagonal K3b reads
+// instead of the per-row diag K2 writes for its own rows only.
+enum { SPLIT_NONE = 0, SPLIT_RCCL = 1, SPLIT_TEST = 2, SPLIT_EMU = 3 };
+struct ScoreSplit {
+    int mode = SPLIT_NONE;
+    int parts = 1, part = 0;
+};
+
+ScoreSplit score_split(const bk_ctx *c, int64_t n) {
+    ScoreSplit s;
+    if (!c->comm || c->split_min_n <= 0 || n < c->split_min_n || !scores_transposed((int)n))
+        return s;
+    if (c->nranks > 1) {
+        s.mode = SPLIT_RCCL;
+        s.parts = c->nranks;
+        s.part = c->rank;
+    } else if (c->test_split_scores > 1) {
+        s.mode = SPLIT_TEST;
+        s.parts = c->test_split_scores;
+    } else if (c->emu_split_scores > 1) {
+        s.mode = SPLIT_EMU;
+        s.parts = c->emu_split_scores;
     }
+    return s;
+}
+
+// stage_finish's workspace, allocated before a sharded call's exchange so that
+// a failure is caught by the ranks' status agreement: with split scoring
+// stage_finish holds a collective, which no rank may skip
+int prepare_finish(bk_ctx *c, int64_t n, const ScoreSplit &sp, bool own_scores) {
+    CHK(ensure(c->mask, (size_t)n * sizeof(int)));
+    if (own_scores) CHK(ensure(c->scores, (size_t)n * sizeof(double)));
     CHK(ensure(c->diag, (size_t)n * sizeof(double)));
     CHK(ensure(c->bnd, 2 * sizeof(double)));
     CHK(margin_rec(c));
+    const int T = (int)((n + 63) / 64);
+    if (scores_transposed((int)n))
+        CHK(ensure(c->Ut, ((size_t)T * (T + 1) / 2 * 4096 + (size_t)T * 64) * sizeof(double)));
+    if (sp.parts > 1) {  // the slices, then K3b's 3-word record
+        const int64_t ch = (n + sp.parts - 1) / sp.parts;
+        CHK(ensure(c->sgather, ((size_t)(ch + 1) * sp.parts + 3) * sizeof(double)));
+    }
+    return BK_OK;
+}
+
+// K2 + K3 + K4 from a packed upper Gram
+int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int dtype,
+                 int64_t n, int64_t d, int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
+                 double *d_mean, const ScoreSplit &sp = ScoreSplit()) {
+    CHK(prepare_finish(c, n, sp, d_scores == nullptr));
+    double *sc = d_scores ? d_scores : (double *)c->scores.p;
     int *mask = (int *)c->mask.p;
     double *diag = (double *)c->diag.p, *bnd = (double *)c->bnd.p;
     const int64_t m = n - f;
@@ -572,21 +633,88 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     // Gram error, totals after an exchange
     const double *dcols = U + (size_t)pl.ntile * 4096;
     const double *Ut = nullptr, *dg = nullptr;
+    int st = BK_OK;
     if (scores_transposed((int)n)) {
         // large n: transposed off-diagonal tiles + contiguous diagonal, so K2
         // reads rows in 512-B runs (the packed upper's lower half is strided)
         const size_t tiles = (size_t)pl.ntile * 4096;
-        CHK(ensure(c->Ut, (tiles + (size_t)pl.T * 64) * sizeof(double)));
         double *ut = (double *)c->Ut.p;
-        CHK(timed(c, BK_K_EXPAND,
-                  [&] { return launch_transpose(U, pl.T, ut, ut + tiles, c->stream); }));
+        st = timed(c, BK_K_EXPAND, [&] { return launch_transpose(U, pl.T, ut, ut + tiles, c->stream); });
         Ut = ut;
         dg = ut + tiles;
     }
-    CHK(timed(c, BK_K_SCORES,
-              [&] { return launch_scores(U, Ut, dg, pl.T, (int)n, k, sc, diag, c->stream); }));
-    CHK(timed(c, BK_K_RANK,
-              [&] { return launch_rank(sc, (int)n, (int)m, mask, bnd, c->stream); }));
+    if (sp.parts <= 1) {
+        CHK(st);
+        CHK(timed(c, BK_K_SCORES,
+                  [&] { return launch_scores(U, Ut, dg, pl.T, (int)n, k, sc, diag, c->stream); }));
+        CHK(timed(c, BK_K_RANK,
+                  [&] { return launch_rank(sc, (int)n, (int)m, mask, bnd, c->stream); }));
+    } else {
+        const int64_t ch = (n + sp.parts - 1) / sp.parts;
+        double *sg = (double *)c->sgather.p;
+        // part p's K2 writes scores[i] of its rows through sg + p, i.e. at
+        // p (ch + 1) + (i - p ch); its status word follows at p (ch + 1) + ch
+        auto share = [&](int p, bool ok) {
+            const int64_t r0 = (int64_t)p * ch, r1 = r0 + ch < n ? r0 + ch : n;
+            int s2 = ok ? BK_OK : BK_EHIP;
+            if (s2 == BK_OK && r1 > r0)
+                s2 = timed(c, BK_K_SCORES, [&] {
+                    return launch_scores(U, Ut, dg, pl.T, (int)n, k, sg + p, diag, c->stream,
+                                         (int)r0, (int)(r1 - r0));
+                });
+            const hipError_t e = hipMemsetAsync(sg + (size_t)p * (ch + 1) + ch, s2 == BK_OK ? 0 : 0xFF,
+                                                sizeof(double), c->stream);
+            if (s2 == BK_OK && e != hipSuccess)
+                s2 = fail(BK_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+            return s2;
+        };
+        if (sp.mode == SPLIT_RCCL) {
+            // every rank joins the all-gather, whatever happened to its share
+            const std::string pre = st == BK_OK ? std::string() : g_err;
+            const int s2 = share(sp.part, st == BK_OK);
+            if (st == BK_OK) st = s2;
+            const std::string msg = st == BK_OK ? std::string() : (pre.empty() ? g_err : pre);
+            hipEvent_t a = nullptr, b = nullptr;
+            const bool ton = timing_on(c, BK_K_SCORE_GATHER);
+            if (ton) {
+                CHK(get_event(c, &a));
+                CHK(get_event(c, &b));
+                HIPCHK(hipEventRecord(a, c->stream));
+            }
+            RCCLCHK(ncclAllGather(sg + (size_t)sp.part * (ch + 1), sg, (size_t)(ch + 1), ncclDouble,
+                                  c->comm, c->stream));
+            if (ton) {
+                HIPCHK(hipEventRecord(b, c->stream));
+                c->pending.push_back({BK_K_SCORE_GATHER, a, b});
+            }
+            if (st != BK_OK) {
+                g_err = msg;
+                return st;
+            }
+        } else {
+            CHK(st);
+            // one GPU standing in for the ranks: every share (test), or rank
+            // 0's once a mode's first call has scored them all (timing
+            // emulation: the other shares' scores are that first call's)
+            const bool all = sp.mode == SPLIT_TEST || c->emu_split_n != n;
+            for (int p = 0; p < sp.parts; ++p) {
+                // (test: a share that "fails" is another rank's failure seen
+                // from this one -- its NaN status poisons the record below)
+                const bool ok = !(sp.mode == SPLIT_TEST && c->test_split_fail == p + 1);
+                if (all || p == 0) {
+                    const int s2 = share(p, ok);
+                    if (ok) CHK(s2);
+                }
+            }
+            if (sp.mode == SPLIT_EMU) c->emu_split_n = n;
+        }
+        double *rec = sg + (size_t)(ch + 1) * sp.parts;
+        HIPCHK(launch_split_unpack(sg, ch, sp.parts, (int)n, dcols, sc, rec, c->stream));
+        dcols = rec;
+        CHK(timed(c, BK_K_RANK,
+                  [&] { return launch_rank(sc, (int)n, (int)m, mask, bnd, c->stream); }));
+        diag = const_cast<double *>(dg);  // K2 wrote only its own rows' diag
+    }
     CHK(timed(c, BK_K_COMPACT, [&] {
         return launch_compact(mask, (int)n, d_sel, diag, bnd, dcols, k, c->dmargin, c->stream);
     }));
@@ -1170,6 +1298,10 @@ int bk_create(bk_ctx **out, int device) {
     if (const char *v = getenv("BK_SMALL_CHECK_LINES")) c->small_check_lines = atoi(v) != 0;
     if (const char *v = getenv("BK_TEST_FAIL_BEFORE_EXCHANGE")) c->test_fail_exchange = atoi(v);
     if (const char *v = getenv("BK_TEST_I8_ENOMEM")) c->test_i8_enomem = atoi(v) != 0;
+    if (const char *v = getenv("BK_SPLIT_SCORES_MIN_N")) c->split_min_n = atoll(v);
+    if (const char *v = getenv("BK_TEST_SPLIT_SCORES")) c->test_split_scores = atoi(v);
+    if (const char *v = getenv("BK_EMU_SPLIT_SCORES")) c->emu_split_scores = atoi(v);
+    if (const char *v = getenv("BK_TEST_SPLIT_FAIL")) c->test_split_fail = atoi(v);
     e = configure_kernels();
     if (e == hipSuccess) e = configure_aggregate_kernels();
     if (e == hipSuccess) e = configure_i8_kernels();
@@ -1193,7 +1325,7 @@ void bk_destroy(bk_ctx *c) {
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                           &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
                           &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws,
-                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws};
+                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws, &c->sgather};
         if (c->hmargin) (void)hipHostFree(c->hmargin);
         if (c->hout) (void)hipHostFree(c->hout);
         if (c->copy) (void)hipStreamSynchronize(c->copy);
@@ -1376,6 +1508,7 @@ int bk_set_f32_mode(bk_ctx *c, int mode) {
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f32_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
     c->f32_mode = mode;
+    c->emu_split_n = -1;  // BK_EMU_SPLIT_SCORES: the new mode's first call scores every share
     return BK_OK;
 }
 
@@ -1387,6 +1520,7 @@ int bk_set_f64_mode(bk_ctx *c, int mode) {
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f64_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
     c->f64_mode = mode;
+    c->emu_split_n = -1;
     return BK_OK;
 }
 
@@ -1590,9 +1724,11 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
     const bool agree = exch && (c->nranks > 1 || c->test_fail_exchange) &&
                        (n != c->agreed_n || f != c->agreed_f || dtype != c->agreed_dtype ||
                         c->deterministic != c->agreed_det);
+    const ScoreSplit sp = score_split(c, n);
     int prep = ensure(c->U, (size_t)usz * sizeof(double));
     if (prep == BK_OK && exch && c->deterministic)
         prep = ensure(c->Ug, (size_t)usz * c->nranks * sizeof(double));
+    if (prep == BK_OK && sp.parts > 1) prep = prepare_finish(c, n, sp, d_scores == nullptr);
     if (prep == BK_OK && dl > 0) prep = prepare_gram(c, dX, dtype, n, dl, ld);
     if (prep == BK_OK && c->test_fail_exchange == (agree ? 1 : 2))
         prep = fail(BK_ENOMEM, "test knob BK_TEST_FAIL_BEFORE_EXCHANGE=%d: forced failure",
@@ -1661,12 +1797,12 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
     }
     if (st != BK_OK) {
         // the rest of the finish still runs, so this rank's record says so too
-        (void)stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, nullptr);
+        (void)stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, nullptr, sp);
         g_err = st_msg;
         return st;
     }
     return stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores,
-                        dl > 0 ? d_mean : nullptr);
+                        dl > 0 ? d_mean : nullptr, sp);
 }
 }  // namespace
 

@@ -114,12 +114,19 @@ hipError_t launch_sum_ranks(const double *Ug, int R, int64_t stride, double *U, 
 hipError_t launch_add_upper(double *U, const double *P, int64_t count, hipStream_t st);
 // Ut / dg: nullable (large n: k_transpose's transposed off-diagonal tiles and
 // contiguous diagonal, for coalesced row reads)
+// r0 / rows: score rows [r0, r0 + rows) only (rows < 0: to n), writing scores[i]
+// and diag[i] for those rows (split scoring over the ranks of a sharded call)
 hipError_t launch_scores(const double *U, const double *Ut, const double *dg, int T, int n,
-                         int64_t k, double *scores, double *diag, hipStream_t st);
+                         int64_t k, double *scores, double *diag, hipStream_t st, int r0 = 0,
+                         int rows = -1);
 bool scores_transposed(int n);
 hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipStream_t st);
 hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bnd,
                        hipStream_t st);
+// split scoring: gathered {ch scores, status} slices -> n contiguous scores,
+// and rec = dcols[0..2] (NaN when a rank's status is not 0)
+hipError_t launch_split_unpack(const double *sg, int64_t ch, int parts, int n, const double *dcols,
+                               double *scores, double *rec, hipStream_t st);
 // The device margin record: MARGIN_WORDS doubles, the public 8 (bk.h
 // bk_selection_margin_record) then u_G.  margin[2] codes besides 0 / 1 mark
 // the call's outputs invalid (read_margin turns them into errors):

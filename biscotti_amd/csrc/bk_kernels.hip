@@ -1315,11 +1315,13 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
                                                 const double *__restrict__ Ut,
                                                 const double *__restrict__ dg_in, int T_, int n,
                                                 int N, int64_t k, double *__restrict__ scores,
-                                                double *__restrict__ diag) {
+                                                double *__restrict__ diag, int r0) {
     static_assert(NT_SUM % NT == 0 && NT % 64 == 0, "summation shape");
     extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // N
     __shared__ double red[NT_SUM / 64];
-    const int i = blockIdx.x, tid = threadIdx.x;
+    // row i: workgroup b scores row r0 + b (a rank's share of the rows when the
+    // scoring is split over the ranks of a sharded call; r0 = 0 otherwise)
+    const int i = r0 + (int)blockIdx.x, tid = threadIdx.x;
     const double di = TR ? dg_in[i] : u_at(U, T_, i, i);
     if (tid == 0) diag[i] = di;
     // distances, element e = tid + NT q (consecutive lanes, consecutive
@@ -1693,7 +1695,8 @@ static int next_pow2(int v) {
 
 template <int NT, int KPT, int NT_SUM, bool TR>
 static void launch_scores2(const double *U, const double *Ut, const double *dg, int T, int n, int N,
-                           int64_t k, double *scores, double *diag, hipStream_t st) {
+                           int64_t k, double *scores, double *diag, hipStream_t st, int r0,
+                           int rows) {
     const size_t lds = (size_t)(KPT == 16 ? N + N / 16 : N) * sizeof(uint64_t);  // v3: padded
     if constexpr (kProbes) {  // timing-only ablations (tools/k2_modes.py): probe builds only
         static const int mode = [] {
@@ -1701,18 +1704,18 @@ static void launch_scores2(const double *U, const double *Ut, const double *dg, 
             return e ? atoi(e) : 0;
         }();
         if (mode == 1) {
-            hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 1>), dim3(n), dim3(NT), lds, st, U,
-                               Ut, dg, T, n, N, k, scores, diag);
+            hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 1>), dim3(rows), dim3(NT), lds, st,
+                               U, Ut, dg, T, n, N, k, scores, diag, r0);
             return;
         }
         if (mode == 2) {
-            hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 2>), dim3(n), dim3(NT), lds, st, U,
-                               Ut, dg, T, n, N, k, scores, diag);
+            hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR, 2>), dim3(rows), dim3(NT), lds, st,
+                               U, Ut, dg, T, n, N, k, scores, diag, r0);
             return;
         }
     }
-    hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR>), dim3(n), dim3(NT), lds, st, U, Ut, dg, T,
-                       n, N, k, scores, diag);
+    hipLaunchKernelGGL((k_scores2<NT, KPT, NT_SUM, TR>), dim3(rows), dim3(NT), lds, st, U, Ut, dg,
+                       T, n, N, k, scores, diag, r0);
 }
 
 bool scores_transposed(int n) {
@@ -1730,7 +1733,11 @@ hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipS
 }
 
 hipError_t launch_scores(const double *U, const double *Ut, const double *dg, int T, int n,
-                         int64_t k, double *scores, double *diag, hipStream_t st) {
+                         int64_t k, double *scores, double *diag, hipStream_t st, int r0,
+                         int rows) {
+    if (rows < 0) rows = n - r0;
+    if (r0 < 0 || rows < 0 || r0 + rows > n) return hipErrorInvalidValue;
+    if (rows == 0) return hipSuccess;
     const int np2 = next_pow2(n < 2 ? 2 : n);
     const size_t lds = (size_t)np2 * sizeof(uint64_t);
     static const bool v1 = [] {
@@ -1745,35 +1752,39 @@ hipError_t launch_scores(const double *U, const double *Ut, const double *dg, in
         // v2: 256 threads up to 2048 keys (KPT = N / 256), then KPT = 16 (or
         // 4); the v1 summation shape (256 / 1024 threads) is emulated
         const int N = np2 < 256 ? 256 : np2;
+#define BK_K2(NT, KPT, NS, TR) \
+    launch_scores2<NT, KPT, NS, TR>(U, Ut, dg, T, n, N, k, scores, diag, st, r0, rows)
         if (Ut) {
             switch (N) {
             case 4096:
                 if (kpt_big == 4)
-                    launch_scores2<1024, 4, 1024, true>(U, Ut, dg, T, n, N, k, scores, diag, st);
+                    BK_K2(1024, 4, 1024, true);
                 else
-                    launch_scores2<256, 16, 1024, true>(U, Ut, dg, T, n, N, k, scores, diag, st);
+                    BK_K2(256, 16, 1024, true);
                 break;
-            case 8192: launch_scores2<512, 16, 1024, true>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
-            default: launch_scores2<1024, 16, 1024, true>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
+            case 8192: BK_K2(512, 16, 1024, true); break;
+            default: BK_K2(1024, 16, 1024, true); break;
             }
-            return hipGetLastError();
+        } else {
+            switch (N) {
+            case 256: BK_K2(256, 1, 256, false); break;
+            case 512: BK_K2(256, 2, 256, false); break;
+            case 1024: BK_K2(256, 4, 256, false); break;
+            case 2048: BK_K2(256, 8, 256, false); break;
+            case 4096:
+                if (kpt_big == 4)
+                    BK_K2(1024, 4, 1024, false);
+                else
+                    BK_K2(256, 16, 1024, false);
+                break;
+            case 8192: BK_K2(512, 16, 1024, false); break;
+            default: BK_K2(1024, 16, 1024, false); break;
+            }
         }
-        switch (N) {
-        case 256: launch_scores2<256, 1, 256, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
-        case 512: launch_scores2<256, 2, 256, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
-        case 1024: launch_scores2<256, 4, 256, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
-        case 2048: launch_scores2<256, 8, 256, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
-        case 4096:
-            if (kpt_big == 4)
-                launch_scores2<1024, 4, 1024, false>(U, Ut, dg, T, n, N, k, scores, diag, st);
-            else
-                launch_scores2<256, 16, 1024, false>(U, Ut, dg, T, n, N, k, scores, diag, st);
-            break;
-        case 8192: launch_scores2<512, 16, 1024, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
-        default: launch_scores2<1024, 16, 1024, false>(U, Ut, dg, T, n, N, k, scores, diag, st); break;
-        }
+#undef BK_K2
         return hipGetLastError();
     }
+    if (r0 != 0 || rows != n) return hipErrorInvalidValue;  // v1 (probe builds): whole calls only
     if (np2 <= 2048) {
         hipLaunchKernelGGL(k_scores<256>, dim3(n), dim3(256), lds, st, U, T, n, np2, k, scores,
                            diag);
@@ -1787,6 +1798,33 @@ hipError_t launch_scores(const double *U, const double *Ut, const double *dg, in
 hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bnd,
                        hipStream_t st) {
     hipLaunchKernelGGL(k_rank, dim3((n + 3) / 4), dim3(256), 0, st, scores, n, m, mask, bnd);
+    return hipGetLastError();
+}
+
+// split scoring (bk_api.hip stage_finish): the gathered slices {ch scores,
+// status} of `parts` ranks -> the n scores, contiguous; rec = the Gram's
+// trailing record dcols[0..2], or NaN words when any rank's status is not 0
+__global__ __launch_bounds__(256) void k_split_unpack(const double *__restrict__ sg, int64_t ch,
+                                                      int parts, int n,
+                                                      const double *__restrict__ dcols,
+                                                      double *__restrict__ scores,
+                                                      double *__restrict__ rec) {
+    const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (i < n) scores[i] = sg[i + i / ch];
+    if (blockIdx.x != 0) return;
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    for (int p = (int)threadIdx.x; p < parts; p += 256)
+        if (sg[(int64_t)p * (ch + 1) + ch] != 0.0) bad = 1;  // NaN compares unequal too
+    __syncthreads();
+    if (threadIdx.x < 3) rec[threadIdx.x] = bad ? __builtin_nan("") : dcols[threadIdx.x];
+}
+
+hipError_t launch_split_unpack(const double *sg, int64_t ch, int parts, int n, const double *dcols,
+                               double *scores, double *rec, hipStream_t st) {
+    hipLaunchKernelGGL(k_split_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sg, ch,
+                       parts, n, dcols, scores, rec);
     return hipGetLastError();
 }
 

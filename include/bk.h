@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 11
+#define BK_ABI_VERSION 12
 
 typedef struct bk_ctx bk_ctx;
 
@@ -462,7 +462,8 @@ enum bk_kernel_id {
     BK_K_RONI = 14,      /* K7  RONI counts + scores (bk_roni*)                 */
     BK_K_SMALL = 15,     /* K1..K4 fused in one launch for n <= 128 (k_small)   */
     BK_K_SLICE = 16,     /* K1i8 digit slicing + error bound (BK_F32_I8)        */
-    BK_NUM_KERNELS = 17
+    BK_K_SCORE_GATHER = 17, /* C2 RCCL all-gather of the split scores (n >= 2049) */
+    BK_NUM_KERNELS = 18
 };
 int bk_timing_enable(bk_ctx *ctx, int on);   /* all kernels; clears accumulated timings */
 /* Time only the kernels whose bit (1u << kernel_id) is set: every timed kernel

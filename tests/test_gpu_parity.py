@@ -362,3 +362,86 @@ def test_concurrent_callers_one_context_and_two(oracle):
     e1.close()
     e2.close()
     assert not errors, errors
+
+
+def _split_engine(monkeypatch, parts, fail=0):
+    """A 1-rank RCCL communicator that scores in `parts` row shares, as that
+    many ranks would (BK_TEST_SPLIT_SCORES; read at bk_create)."""
+    from biscotti_amd.krum import Engine, comm_unique_id
+    monkeypatch.setenv("BK_TEST_SPLIT_SCORES", str(parts))
+    if fail:
+        monkeypatch.setenv("BK_TEST_SPLIT_FAIL", str(fail))
+    e = Engine(0)
+    monkeypatch.delenv("BK_TEST_SPLIT_SCORES")
+    monkeypatch.delenv("BK_TEST_SPLIT_FAIL", raising=False)
+    e.set_stream(torch.cuda.current_stream().cuda_stream)
+    e.comm_init(1, 0, comm_unique_id())
+    return e
+
+
+@pytest.mark.parametrize("parts", [2, 3, 8])
+@pytest.mark.parametrize("own_scores", [False, True])
+def test_split_scores_bitwise(engine, monkeypatch, parts, own_scores):
+    """Split scoring (n >= 2049 on the sharded entry: each rank scores its
+    ceil(n / R) rows, one all-gather hands every rank all n scores): the R
+    shares computed as R ranks would, on one GPU, give the unsplit call's
+    selection, scores, mean and margin record bitwise -- with the caller's
+    scores array or without one (libbk's own)."""
+    e2 = _split_engine(monkeypatch, parts)
+    try:
+        n, d, f = 2100, 3000, 630
+        X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+        engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 17, f)
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        sc = torch.empty(n, dtype=torch.float64, device="cuda")
+        mean = torch.empty(d, dtype=torch.float64, device="cuda")
+        e2.timing_enable(True)
+        for _ in range(2):
+            e2.multikrum_sharded_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr(),
+                                     None if own_scores else sc.data_ptr(), mean.data_ptr())
+        e2.synchronize()
+        t = e2.timing_read()
+        e2.timing_enable(False)
+        assert t["k_scores"]["count"] == 2 * parts  # one launch per share
+        fsel, fsc, fmean = _dev_run(engine, X, f)
+        assert np.array_equal(sel.cpu().numpy(), fsel)
+        if not own_scores:
+            assert np.array_equal(sc.cpu().numpy().view(np.int64), fsc.view(np.int64))
+        assert np.array_equal(mean.cpu().numpy().view(np.int64), fmean.view(np.int64))
+        m2, m1 = e2.selection_margin(), engine.selection_margin()
+        assert m2 == m1
+    finally:
+        e2.close()
+
+
+def test_split_scores_below_threshold_and_failed_share(engine, monkeypatch):
+    """n = 2048 stays on one K2 launch (the split needs the transposed path);
+    a share that fails on another rank marks the call invalid on this one
+    (its NaN status word poisons the Gram record: BK_ERCCL, as a shard that
+    fails before the exchange)."""
+    e2 = _split_engine(monkeypatch, 4)
+    try:
+        n, d, f = 2048, 1000, 614
+        X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+        engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 19, f)
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        e2.timing_enable(True)
+        e2.multikrum_sharded_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr())
+        e2.synchronize()
+        assert e2.timing_read()["k_scores"]["count"] == 1
+        e2.timing_enable(False)
+        assert np.array_equal(sel.cpu().numpy(), _dev_run(engine, X, f)[0])
+    finally:
+        e2.close()
+    e3 = _split_engine(monkeypatch, 3, fail=2)
+    try:
+        n, d, f = 2100, 1000, 630
+        X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+        engine.synth_fill_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, 0, d, 23, f)
+        sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+        e3.multikrum_sharded_ptr(X.data_ptr(), _lib.BK_F64, n, d, d, f, sel.data_ptr())
+        with pytest.raises(_lib.BKError) as ei:
+            e3.synchronize()
+        assert ei.value.status == _lib.BK_ERCCL
+    finally:
+        e3.close()
