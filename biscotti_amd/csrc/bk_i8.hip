@@ -580,6 +580,9 @@ __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ pa
 // short of full, R is raised (in eights, up to 4x, ranges >= 16 chunks) to the
 // count that fills the rounds (config D: 10 tiles x 64 ranges = 2.5 rounds of
 // 32 CUs per XCD -> 128 ranges, 5 rounds; config E stays at 8: 16.5 of 17)
+#ifndef BK_I8_RQ
+#define BK_I8_RQ 8  // column ranges come in multiples of this (A/B builds)
+#endif
 I8Layout i8_layout(int n, int64_t d, int es, int num_cu, int ns) {
     I8Layout L;
     L.ns = ns == 2 ? 2 : 3;
@@ -601,20 +604,44 @@ I8Layout i8_layout(int n, int64_t d, int es, int num_cu, int ns) {
                 for (int J = BJ * SBJ; J < BJ * SBJ + SBJ && J < TJn; ++J)
                     if (I <= rj * J + rj - 1) tiles.push_back(I | J << 16);
     const int NT = (int)tiles.size();
-    int64_t R = (L.dp + cmax - 1) / cmax;
-    R = (R + 7) / 8 * 8;
+    const int64_t R0 = (L.dp + cmax - 1) / cmax;  // the fewest ranges the slice width allows
+    int64_t R = (R0 + BK_I8_RQ - 1) / BK_I8_RQ * BK_I8_RQ;
     R = nk < R ? nk : R;
-    {
+    const int ncu = num_cu > 0 ? num_cu : 256;
+    if (R0 < BK_I8_RQ) {
+        // short rows (one rank's shard of a d-sharded call, e.g. E at 8 GPUs:
+        // 32,768 columns): every range of a tile is one workgroup that pays a
+        // fixed cost (pipeline fill, the 128 x tj partial it writes, its share
+        // of k_i8_reduce), so fewer, longer ranges win until the grid gets
+        // short of workgroups.  cost(R) = workgroup rounds x (columns per
+        // range + C0) + C1 R, in columns, C1 growing as the n^2 partials each
+        // range adds to k_i8_reduce; C0 = 2048 and C1 = 3072 at n = 4096
+        // fitted over E's 8- and 4-rank shards, two and three digits
+        // (profiles/r05/ab_i8_ranges.log: within 2 % of the best R measured,
+        // 1.1-1.5x faster than the 8 ranges of before)
+        const double c1 = 3072.0 * ((double)n / 4096.0) * ((double)n / 4096.0);
+        auto cost = [&](int64_t r) {
+            const double rounds = std::ceil((double)NT * r / ncu);
+            return rounds * ((double)L.dp / r + 2048.0) + c1 * r;
+        };
+        int64_t best = R0;
+        for (int64_t r = R0 + 1; r <= BK_I8_RQ && r <= nk; ++r)
+            if (cost(r) < cost(best)) best = r;
+        R = best;
+    } else {
         const double cx = num_cu > 0 ? num_cu / 8.0 : 32.0;  // CUs per XCD
         auto eff = [&](int64_t r) {
             const double rounds = (double)((NT * r + 7) / 8) / cx;
             return rounds / std::ceil(rounds);
         };
         int64_t best = R;
-        for (int64_t r = R + 8; r <= 4 * R && nk / r >= 16; r += 8)
+        for (int64_t r = R + BK_I8_RQ; r <= 4 * R && nk / r >= 16; r += BK_I8_RQ)
             if (eff(r) > eff(best) + 0.05) best = r;
         R = best;
     }
+#ifdef BK_I8_RFIX
+    R = BK_I8_RFIX < nk ? BK_I8_RFIX : nk;  // A/B builds: a fixed range count
+#endif
     L.R = (int)R;
     L.es = es;
     L.rb.resize(L.R + 1);

@@ -60,17 +60,29 @@ def _ntiles(n, ns):
 
 
 def _ranges(n, d, es, num_cu=256, ns=3):
-    """bk_i8.hip i8_layout: R column ranges of whole 64-column granules, at
-    least 8, in eights, each row slice <= 128 KiB; then raised (in eights, up
-    to 4x, ranges >= 16 chunks) when that fills the XCDs' last round of
-    (tile, range) workgroups by more than 5 points."""
+    """bk_i8.hip i8_layout: R column ranges of whole 64-column granules, each
+    row slice <= 128 KiB.  Rows that need fewer than 8 such ranges (a shard of
+    a d-sharded call): R in [R0, 8] minimising workgroup rounds x (columns per
+    range + 2048) + 3072 (n / 4096)^2 R.  Otherwise at least 8, in eights;
+    then raised (in eights, up to 4x, ranges >= 16 chunks) when that fills the
+    XCDs' last round of (tile, range) workgroups by more than 5 points."""
     dp = (d + 63) // 64 * 64
     nk = dp // 64
     cmax = 131072 // es
-    R = -(-dp // cmax)
-    R = -(-R // 8) * 8
-    R = min(nk, R)
+    R0 = -(-dp // cmax)
     NT = _ntiles(n, ns)
+    if R0 < 8:
+        c1 = 3072.0 * (n / 4096.0) * (n / 4096.0)
+
+        def cost(r):
+            return math.ceil(NT * r / num_cu) * (dp / r + 2048.0) + c1 * r
+        R = R0
+        for r in range(R0 + 1, min(8, nk) + 1):
+            if cost(r) < cost(R):
+                R = r
+        return [(nk * r // R * 64, nk * (r + 1) // R * 64) for r in range(R)]
+    R = -(-R0 // 8) * 8
+    R = min(nk, R)
     cx = num_cu / 8.0
 
     def eff(r):
