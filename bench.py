@@ -822,6 +822,8 @@ def _summ(v, host=None):
          "near_tie": (par.get("margin") or {}).get("near_tie")}
     if "certified_reruns" in v:
         s["reruns"] = v["certified_reruns"]
+    if "error" in v:
+        s["error"] = v["error"]
     if "per_rank" in v:  # a d-sharded variant: the slowest rank's exchange and score gather
         s["exchange_ms"] = v.get("exchange_ms")
         s["score_gather_ms"] = v.get("score_gather_ms")
@@ -1221,8 +1223,14 @@ def main():
         # config E at this rank count (BASELINE: fp32, 8 x MI355X), each rank
         # its own column shard, beside the headline D (d-sharded the same way)
         for mode in E_SHARD_MODES:
-            variants[workload_tag("E_4096x262144_fp32", mode)] = sharded_variant(
-                eng, dev, "E_4096x262144_fp32", mode, emu or world, rank, world, barrier, emu)
+            tag = workload_tag("E_4096x262144_fp32", mode)
+            try:
+                variants[tag] = sharded_variant(eng, dev, "E_4096x262144_fp32", mode, emu or world,
+                                                rank, world, barrier, emu)
+            except Exception as e:  # noqa: BLE001 -- a variant's failure must not cost the headline line
+                log("bench.py: sharded variant %s failed: %r" % (tag, e))
+                variants[tag] = {"error": repr(e)}
+                break  # the ranks may no longer be in step: no further collective variants
 
     # roofline of the dominant kernel (K1, fp64 MFMA): algorithmic flops per
     # launch = n(n+1) * d_local (symmetric Gram incl. diagonal)
