@@ -411,6 +411,61 @@ def sharded_variant(eng, dev, name, f32_mode, nparts, rank, world, barrier, emu,
     return out
 
 
+def replica_variant(eng, dev, name, world, barrier, steps=20, warmup=5):
+    """SURVEY §8(e) 'Replicas' -- the reference's own multi-instance pattern
+    (N independent verifiers, DistSys/main.go:1680-1682): every rank runs the
+    WHOLE batch on its own GPU through the single-GPU entry, no collective in
+    the step.  Timed like the headline (barrier, K steps, barrier, max over
+    ranks); value = N batches / step time (weak scaling), each rank's
+    selection checked against the golden."""
+    import hashlib
+    import torch
+    import torch.distributed as tdist
+    from biscotti_amd import _lib
+    w = WORKLOADS[name]
+    n, d, f = w["n"], w["d"], w["f"]
+    m = n - f
+    bdt = _lib.BK_F32 if w["dtype"] == "f32" else _lib.BK_F64
+    es = 4 if w["dtype"] == "f32" else 8
+    X = torch.empty((n, d), dtype=torch.float32 if es == 4 else torch.float64, device=dev)
+    eng.synth_fill_ptr(X.data_ptr(), bdt, n, d, X.stride(0), 0, d, w["seed"], w["nbyz"],
+                       flags=w.get("flags", 0))
+    sel = torch.empty(m, dtype=torch.int64, device=dev)
+    mean = torch.empty(d, dtype=torch.float64, device=dev)
+
+    def step():
+        eng.multikrum_device_ptr(X.data_ptr(), bdt, n, d, X.stride(0), f, sel.data_ptr(), None,
+                                 mean.data_ptr())
+    for _ in range(max(5, warmup)):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    el = max_over_ranks(time.perf_counter() - t0, dev) if world > 1 else time.perf_counter() - t0
+    ms = el / steps * 1e3
+    par = golden_check(name, sel.cpu().numpy(), mean.cpu().numpy(), 0, d) or {}
+    oks = [par.get("selected_set")]
+    h = hashlib.sha256(sel.cpu().numpy().tobytes()).hexdigest()[:16]
+    hs = [h]
+    if world > 1:
+        oks, hs = [None] * world, [None] * world
+        tdist.all_gather_object(oks, par.get("selected_set"))
+        tdist.all_gather_object(hs, h)
+    del X
+    torch.cuda.empty_cache()
+    return {"n": n, "d": d, "f": f, "m": m, "replicas": world, "scaling": "weak",
+            "parallelism": "%d independent replicas (no collective)" % world,
+            "steps": steps, "ms_per_step": round(ms, 4),
+            "value": round(world * n * d * es / (ms * 1e-3) / 1e9, 3), "unit": "GB/s",
+            "parity": dict(par, every_rank=oks), "ranks_agree": len(set(hs)) == 1}
+
+
 def host_entry_variant(eng, dev, name, steps=200, warmup=20, single_calls=7, idle_s=0.2):
     """What a Biscotti verifier's own call costs (krum.go:100-166: the batch
     arrives over RPC into host slices): bk_multikrum(BK_HOST_PINNED) from a
@@ -824,6 +879,9 @@ def _summ(v, host=None):
         s["reruns"] = v["certified_reruns"]
     if "error" in v:
         s["error"] = v["error"]
+    if "replicas" in v:
+        s["replicas"] = v["replicas"]
+        s["ranks_agree"] = v.get("ranks_agree")
     if "per_rank" in v:  # a d-sharded variant: the slowest rank's exchange and score gather
         s["exchange_ms"] = v.get("exchange_ms")
         s["score_gather_ms"] = v.get("score_gather_ms")
@@ -1231,6 +1289,10 @@ def main():
                 log("bench.py: sharded variant %s failed: %r" % (tag, e))
                 variants[tag] = {"error": repr(e)}
                 break  # the ranks may no longer be in step: no further collective variants
+    if world > 1 and not a.no_variants and WORKLOADS[a.workload]["n"] > 128:
+        # the reference's own scale-out: N independent verifiers, one batch each
+        # (no exchange, so it runs under --exchange host too)
+        variants[a.workload + "_replicas"] = replica_variant(eng, dev, a.workload, world, barrier)
 
     # roofline of the dominant kernel (K1, fp64 MFMA): algorithmic flops per
     # launch = n(n+1) * d_local (symmetric Gram incl. diagonal)

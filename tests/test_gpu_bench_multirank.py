@@ -59,12 +59,13 @@ def test_bench_launches_its_own_ranks():
     WORLD_SIZE) starts its own two ranks as a child torch.distributed.run and
     relays rank 0's line: n_gpus 2, both ranks agree on the set, the shard's
     golden matches, and every rank's K1 and exchange time per step are in the
-    line.  The host exchange lets the two ranks share the box's one GPU."""
+    line, with the replicas form (each rank the whole batch, golden on every
+    rank).  The host exchange lets the two ranks share the box's one GPU."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
            "--exchange", "host", "--workload", "C_1024x131072", "--no-cpu-baseline", "--no-e2e",
-           "--no-next-rows", "--no-graph-probe", "--no-variants"]
+           "--no-next-rows", "--no-graph-probe"]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [x for x in r.stdout.splitlines() if x.strip()]
@@ -78,6 +79,9 @@ def test_bench_launches_its_own_ranks():
     assert all(p["k_gram_ms"] > 0 and p["exchange_ms"] > 0 for p in rc["per_rank"]), rc
     assert rc["exchange_ms"] == max(p["exchange_ms"] for p in rc["per_rank"])
     assert sum(p["d_local"] for p in rc["per_rank"]) == out["config"]["d"]
+    # the replicas form: each rank the whole batch, no exchange
+    rep = out["summary"]["C_1024x131072_replicas"]
+    assert rep["sel"] == "match" and rep["value"] > 0, rep
 
 
 def test_bench_refuses_more_rccl_ranks_than_gpus():
