@@ -414,6 +414,44 @@ def test_split_scores_bitwise(engine, monkeypatch, parts, own_scores):
         e2.close()
 
 
+@pytest.mark.parametrize("form", ["f64_deterministic", "f32_i8x2_certified", "f32_mfma"])
+def test_split_scores_other_forms(engine, monkeypatch, form):
+    """Split scoring under the deterministic exchange (all-gather + rank-order
+    sum) and on fp32 rows in the modes config E runs at 8 GPUs (the certified
+    two-digit int8 Gram, the fp32 MFMA): 8 shares give the unsplit call's
+    selection, scores and mean bitwise."""
+    e2 = _split_engine(monkeypatch, 8)
+    try:
+        n, d, f = 2200, 2048, 660
+        f32 = form.startswith("f32")
+        dt = _lib.BK_F32 if f32 else _lib.BK_F64
+        X = torch.empty((n, d), dtype=torch.float32 if f32 else torch.float64, device="cuda")
+        engine.synth_fill_ptr(X.data_ptr(), dt, n, d, d, 0, d, 29, f)
+        mode = {"f32_i8x2_certified": _lib.BK_F32_I8X2_CERTIFIED, "f32_mfma": _lib.BK_F32_MFMA}
+        if form == "f64_deterministic":
+            e2.comm_set_mode(True)
+        outs = []
+        for eng, sharded in ((e2, True), (engine, False)):
+            if f32:
+                eng.set_f32_mode(mode[form])
+            sel = torch.empty(n - f, dtype=torch.int64, device="cuda")
+            sc = torch.empty(n, dtype=torch.float64, device="cuda")
+            mean = torch.empty(d, dtype=torch.float64, device="cuda")
+            try:
+                call = eng.multikrum_sharded_ptr if sharded else eng.multikrum_device_ptr
+                call(X.data_ptr(), dt, n, d, d, f, sel.data_ptr(), sc.data_ptr(), mean.data_ptr())
+                eng.synchronize()
+            finally:
+                eng.set_f32_mode(_lib.BK_F32_EXACT)
+            outs.append((sel.cpu().numpy(), sc.cpu().numpy(), mean.cpu().numpy()))
+        (s1, c1, m1), (s2, c2, m2) = outs
+        assert np.array_equal(s1, s2)
+        assert np.array_equal(c1.view(np.int64), c2.view(np.int64))
+        assert np.array_equal(m1.view(np.int64), m2.view(np.int64))
+    finally:
+        e2.close()
+
+
 def test_split_scores_below_threshold_and_failed_share(engine, monkeypatch):
     """n = 2048 stays on one K2 launch (the split needs the transposed path);
     a share that fails on another rank marks the call invalid on this one
