@@ -94,3 +94,34 @@ def test_verifier_flow_against_oracle(harness, oracle, tmp_path):
             else:
                 assert v == ("accepted" if s in it["accepted"] else "rejected"), (k, s, v)
         assert sum(v == "stale" for v in verdicts.values()) == a - n
+
+
+@pytest.mark.gpu
+def test_nodes_agree_like_localtest(harness, oracle, tmp_path):
+    """The reference's only integration test (DistSys/localTest.sh:47-87): N
+    node processes on one host, then every node's log compared with `cmp`.
+    Here four verifier processes share the GPU, each replaying two Krum rounds
+    of config B's shape (100 peers x 7,850 fp64, threshold 100: no stale or
+    deadline race) through libbk; their logs (peer lines in a fixed order) must
+    be byte-identical, and the accepted set the oracle's."""
+    rows, d = 100, 7850
+    X = oracle.synth(rows, d, 20261017, 30)
+    path = tmp_path / "updates.bin"
+    X.astype("<f8").tofile(path)
+    cmd = [harness, str(path), str(rows), str(d), str(rows), "2000", str(rows), str(rows)]
+    procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for _ in range(4)]
+    logs = []
+    for p in procs:
+        out, err = p.communicate(timeout=120)
+        assert p.returncode == 0, err
+        logs.append("\n".join(sorted(out.splitlines())))
+    assert all(lg == logs[0] for lg in logs[1:])
+    iters, _ = parse(logs[0])
+    sid_row = {sid_of(p): p for p in range(rows)}
+    for k in (1, 2):
+        it = iters[k]
+        assert it["path"] == "threshold" and it["n"] == rows and it["status"] == 0
+        Xb = X[[sid_row[s] for s in it["batch"]]]
+        osel, _, _ = oracle.krum(Xb, it["f"])
+        assert it["accepted"] == [it["batch"][i] for i in osel]
