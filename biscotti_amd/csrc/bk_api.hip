@@ -603,6 +603,10 @@ ScoreSplit score_split(const bk_ctx *c, int64_t n) {
 // a failure is caught by the ranks' status agreement: with split scoring
 // stage_finish holds a collective, which no rank may skip
 int prepare_finish(bk_ctx *c, int64_t n, const ScoreSplit &sp, bool own_scores) {
+    if (sp.parts > 1) {  // first: a rank that fails below can still join the all-gather
+        const int64_t ch = (n + sp.parts - 1) / sp.parts;
+        CHK(ensure(c->sgather, ((size_t)(ch + 1) * sp.parts + 3) * sizeof(double)));
+    }
     CHK(ensure(c->mask, (size_t)n * sizeof(int)));
     if (own_scores) CHK(ensure(c->scores, (size_t)n * sizeof(double)));
     CHK(ensure(c->diag, (size_t)n * sizeof(double)));
@@ -611,18 +615,37 @@ int prepare_finish(bk_ctx *c, int64_t n, const ScoreSplit &sp, bool own_scores) 
     const int T = (int)((n + 63) / 64);
     if (scores_transposed((int)n))
         CHK(ensure(c->Ut, ((size_t)T * (T + 1) / 2 * 4096 + (size_t)T * 64) * sizeof(double)));
-    if (sp.parts > 1) {  // the slices, then K3b's 3-word record
-        const int64_t ch = (n + sp.parts - 1) / sp.parts;
-        CHK(ensure(c->sgather, ((size_t)(ch + 1) * sp.parts + 3) * sizeof(double)));
-    }
     return BK_OK;
+}
+
+// a rank whose finish failed before its share still joins the score
+// all-gather with a NaN status, so its peers mark the call invalid instead of
+// waiting for it.  The gather buffer exists: it is sized by (n, ranks) alone
+// and allocated first, on the call whose signature the ranks agreed on
+void join_failed_share(bk_ctx *c, int64_t n, const ScoreSplit &sp) {
+    const int64_t ch = (n + sp.parts - 1) / sp.parts;
+    if (c->sgather.bytes < ((size_t)(ch + 1) * sp.parts + 3) * sizeof(double)) return;
+    double *sg = (double *)c->sgather.p;
+    (void)hipMemsetAsync(sg + (size_t)sp.part * (ch + 1) + ch, 0xFF, sizeof(double), c->stream);
+    (void)ncclAllGather(sg + (size_t)sp.part * (ch + 1), sg, (size_t)(ch + 1), ncclDouble, c->comm,
+                        c->stream);
 }
 
 // K2 + K3 + K4 from a packed upper Gram
 int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int dtype,
                  int64_t n, int64_t d, int64_t ld, int64_t f, int64_t *d_sel, double *d_scores,
                  double *d_mean, const ScoreSplit &sp = ScoreSplit()) {
-    CHK(prepare_finish(c, n, sp, d_scores == nullptr));
+    {
+        const int pf = prepare_finish(c, n, sp, d_scores == nullptr);
+        if (pf != BK_OK) {
+            if (sp.mode == SPLIT_RCCL) {
+                const std::string msg = g_err;
+                join_failed_share(c, n, sp);
+                g_err = msg;
+            }
+            return pf;
+        }
+    }
     double *sc = d_scores ? d_scores : (double *)c->scores.p;
     int *mask = (int *)c->mask.p;
     double *diag = (double *)c->diag.p, *bnd = (double *)c->bnd.p;
@@ -637,9 +660,11 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     if (scores_transposed((int)n)) {
         // large n: transposed off-diagonal tiles + contiguous diagonal, so K2
         // reads rows in 512-B runs (the packed upper's lower half is strided)
+        // (split scoring: each share transposes only what its rows read, below)
         const size_t tiles = (size_t)pl.ntile * 4096;
         double *ut = (double *)c->Ut.p;
-        st = timed(c, BK_K_EXPAND, [&] { return launch_transpose(U, pl.T, ut, ut + tiles, c->stream); });
+        if (sp.parts <= 1)
+            st = timed(c, BK_K_EXPAND, [&] { return launch_transpose(U, pl.T, ut, ut + tiles, c->stream); });
         Ut = ut;
         dg = ut + tiles;
     }
@@ -652,11 +677,20 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
     } else {
         const int64_t ch = (n + sp.parts - 1) / sp.parts;
         double *sg = (double *)c->sgather.p;
-        // part p's K2 writes scores[i] of its rows through sg + p, i.e. at
-        // p (ch + 1) + (i - p ch); its status word follows at p (ch + 1) + ch
+        // share p: the transposed tiles its rows read (block-columns of rows
+        // [r0, r1), and the whole diagonal), then its K2, which writes
+        // scores[i] of its rows through sg + p, i.e. at p (ch + 1) + (i - p ch);
+        // its status word follows at p (ch + 1) + ch
         auto share = [&](int p, bool ok) {
             const int64_t r0 = (int64_t)p * ch, r1 = r0 + ch < n ? r0 + ch : n;
             int s2 = ok ? BK_OK : BK_EHIP;
+            if (s2 == BK_OK) {
+                const int b0 = r1 > r0 ? (int)(r0 >> 6) : 1, b1 = r1 > r0 ? (int)((r1 - 1) >> 6) : 0;
+                double *ut = const_cast<double *>(Ut);
+                s2 = timed(c, BK_K_EXPAND, [&] {
+                    return launch_transpose(U, pl.T, ut, const_cast<double *>(dg), c->stream, b0, b1);
+                });
+            }
             if (s2 == BK_OK && r1 > r0)
                 s2 = timed(c, BK_K_SCORES, [&] {
                     return launch_scores(U, Ut, dg, pl.T, (int)n, k, sg + p, diag, c->stream,
@@ -674,12 +708,18 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
             const int s2 = share(sp.part, st == BK_OK);
             if (st == BK_OK) st = s2;
             const std::string msg = st == BK_OK ? std::string() : (pre.empty() ? g_err : pre);
+            // (timing is best effort here: nothing may keep a rank from the collective)
             hipEvent_t a = nullptr, b = nullptr;
-            const bool ton = timing_on(c, BK_K_SCORE_GATHER);
+            bool ton = timing_on(c, BK_K_SCORE_GATHER);
             if (ton) {
-                CHK(get_event(c, &a));
-                CHK(get_event(c, &b));
-                HIPCHK(hipEventRecord(a, c->stream));
+                const std::string keep = g_err;
+                ton = get_event(c, &a) == BK_OK && get_event(c, &b) == BK_OK &&
+                      hipEventRecord(a, c->stream) == hipSuccess;
+                if (!ton) {
+                    if (a) c->pool.push_back(a);
+                    if (b) c->pool.push_back(b);
+                    g_err = keep;
+                }
             }
             RCCLCHK(ncclAllGather(sg + (size_t)sp.part * (ch + 1), sg, (size_t)(ch + 1), ncclDouble,
                                   c->comm, c->stream));

@@ -120,7 +120,10 @@ hipError_t launch_scores(const double *U, const double *Ut, const double *dg, in
                          int64_t k, double *scores, double *diag, hipStream_t st, int r0 = 0,
                          int rows = -1);
 bool scores_transposed(int n);
-hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipStream_t st);
+// bj0 / bj1: transpose only the off-diagonal tiles of block-columns bj0..bj1
+// (bj1 < 0: all); the diagonal always
+hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipStream_t st,
+                            int bj0 = 0, int bj1 = -1);
 hipError_t launch_rank(const double *scores, int n, int m, int *mask, double *bnd,
                        hipStream_t st);
 // split scoring: gathered {ch scores, status} slices -> n contiguous scores,

@@ -1383,9 +1383,12 @@ __global__ __launch_bounds__(NT) void k_scores2(const double *__restrict__ U,
 
 // Ut (the off-diagonal upper tiles transposed) and the contiguous diagonal,
 // for K2's coalesced row reads at large n; one 64x64 tile per block through LDS
+// [bj0, bj1]: the off-diagonal tiles transposed are those of block-columns
+// bj0..bj1 only -- the rows [64 bj0, 64 bj1 + 64) a rank scores under split
+// scoring read no others; the diagonal (every row's G_jj) always
 __global__ __launch_bounds__(256) void k_transpose(const double *__restrict__ U, int T_,
                                                    double *__restrict__ Ut,
-                                                   double *__restrict__ dg) {
+                                                   double *__restrict__ dg, int bj0, int bj1) {
     __shared__ double t[64][65];
     int bi, bj;
     tri_decode(blockIdx.x, T_, bi, bj);
@@ -1394,6 +1397,7 @@ __global__ __launch_bounds__(256) void k_transpose(const double *__restrict__ U,
         if (threadIdx.x < 64) dg[bi * 64 + threadIdx.x] = src[threadIdx.x * 65];
         return;
     }
+    if (bj < bj0 || bj > bj1) return;  // block-uniform
     for (int e = threadIdx.x; e < 4096; e += 256) t[e >> 6][e & 63] = src[e];
     __syncthreads();
     double *dst = Ut + (int64_t)blockIdx.x * 4096;
@@ -1726,9 +1730,11 @@ bool scores_transposed(int n) {
     return n >= tmin;
 }
 
-hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipStream_t st) {
+hipError_t launch_transpose(const double *U, int T, double *Ut, double *dg, hipStream_t st,
+                            int bj0, int bj1) {
+    if (bj1 < 0) bj1 = T - 1;
     hipLaunchKernelGGL(k_transpose, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, st, U, T, Ut,
-                       dg);
+                       dg, bj0, bj1);
     return hipGetLastError();
 }
 
