@@ -545,6 +545,110 @@ def host_entry_variant(eng, dev, name, steps=200, warmup=20, single_calls=7, idl
             "parity": par}
 
 
+def rows_entry_variant(eng, dev, name, calls=None, thread_sweep=(1, 2, 4, 8, 16)):
+    """The verifier's real input path: n SEPARATELY
+    allocated host rows (Go's deltas [][]float64, krum.go:100-166) -> result.
+      serial:  the shim's old form -- one thread copies the rows into one
+               pinned batch (go/bk/krum_bk.go's copy loop; here np.stack into a
+               pinned buffer, a C loop of one memcpy per row), then
+               bk_multikrum(BK_HOST_PINNED);
+      rows:    bk_multikrum_rows: libbk packs the rows on its host threads into
+               a pinned ring, each column chunk's H2D + Gram starting as soon
+               as it is packed;
+      pinned:  bk_multikrum(BK_HOST_PINNED) on an already-packed batch (the
+               e2e_pinned figure: no pack at all), for the ratio.
+    Outputs of rows and serial compared bitwise (sel, scores, mean)."""
+    import ctypes
+    import torch
+    from biscotti_amd import _lib
+    w = WORKLOADS[name]
+    n, d, f = w["n"], w["d"], w["f"]
+    m = n - f
+    Xd = torch.empty((n, d), dtype=torch.float64, device=dev)
+    eng.synth_fill_ptr(Xd.data_ptr(), _lib.BK_F64, n, d, d, 0, d, w["seed"], w["nbyz"],
+                       flags=w.get("flags", 0))
+    Xh = torch.empty((n, d), dtype=torch.float64, pin_memory=True)
+    Xh.copy_(Xd)
+    del Xd
+    torch.cuda.empty_cache()
+    Xn = Xh.numpy()
+    rows = []
+    for i in range(n):  # n separate allocations, as n RPC-decoded slices
+        r = np.empty(d, dtype=np.float64)
+        r[:] = Xn[i]
+        rows.append(r)
+    ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
+    L = _lib.lib()
+    outs = {k: (np.empty(m, dtype=np.int64), np.empty(n), np.empty(d)) for k in ("rows", "serial")}
+    mo = ctypes.c_int64(0)
+
+    def pinned_call(o):
+        _lib.check(L.bk_multikrum(eng.ctx, ctypes.c_void_p(Xh.data_ptr()), _lib.BK_HOST_PINNED,
+                                  _lib.BK_F64, n, d, d, f, o[0].ctypes.data, ctypes.addressof(mo),
+                                  o[1].ctypes.data, o[2].ctypes.data))
+
+    def serial_call():
+        np.stack(rows, out=Xn)  # the pack: one thread, one memcpy per row
+        pinned_call(outs["serial"])
+
+    def rows_call():
+        o = outs["rows"]
+        _lib.check(L.bk_multikrum_rows(eng.ctx, ptrs, _lib.BK_F64, n, d, f, o[0].ctypes.data,
+                                       ctypes.addressof(mo), o[1].ctypes.data, o[2].ctypes.data))
+
+    def pack_only():
+        np.stack(rows, out=Xn)
+
+    big = n * d * 8 > (256 << 20)
+    calls = calls or (3 if big else 200 if n * d > 1000 else 2000)
+    warm = 2 if big else 20
+
+    def best(fn):  # big batches: min of `calls` single calls; small: mean of a loop
+        for _ in range(warm):
+            fn()
+        if big:
+            ts = []
+            for _ in range(calls):
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            return min(ts) * 1e3
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            fn()
+        return (time.perf_counter() - t0) / calls * 1e3
+
+    res = {"what": "n separate host rows -> selection + mean on the host (krum.go:100-166)",
+           "n": n, "d": d, "f": f, "calls": calls,
+           "host_threads_default": int(os.environ.get("BK_HOST_THREADS") or
+                                       min(16, os.cpu_count() or 1))}
+    res["pack_serial_ms"] = round(best(pack_only), 4)
+    res["e2e_rows_serial_ms"] = round(best(serial_call), 4)
+    res["e2e_pinned_ms"] = round(best(lambda: pinned_call(outs["serial"])), 4)
+    eng.set_host_threads(0)
+    res["e2e_rows_ms"] = round(best(rows_call), 4)
+    sweep = {}
+    for t in thread_sweep:
+        eng.set_host_threads(t)
+        sweep[str(t)] = round(best(rows_call), 4)
+    eng.set_host_threads(0)
+    res["e2e_rows_ms_by_threads"] = sweep
+    rows_call()
+    serial_call()
+    a, b = outs["rows"], outs["serial"]
+    res["bitwise_same_as_serial"] = {
+        "sel": bool(np.array_equal(a[0], b[0])),
+        "scores": bool(np.array_equal(a[1].view(np.int64), b[1].view(np.int64))),
+        "mean": bool(np.array_equal(a[2].view(np.int64), b[2].view(np.int64)))}
+    res["rows_over_pinned"] = round(res["e2e_rows_ms"] / res["e2e_pinned_ms"], 4)
+    res["serial_over_pinned"] = round(res["e2e_rows_serial_ms"] / res["e2e_pinned_ms"], 4)
+    res["GB_per_s_rows"] = round(n * d * 8 / (res["e2e_rows_ms"] * 1e-3) / 1e9, 3)
+    par = golden_check(name, a[0].copy(), a[2].copy(), 0, d) or {}
+    res["parity"] = par
+    del Xh, rows
+    return res
+
+
 def next_rows(eng, X, n, d, sel, m, steps=5):
     """SURVEY.md §8(f) rows 2-4 on the same device-resident batch (HBM-bound):
     block aggregation of the m selected rows into GlobalW (K4'), the
@@ -940,6 +1044,13 @@ def compact_line(out, detail_path):
     e2e = out.get("e2e_pinned_h2d_d2h")
     if e2e:
         summ["e2e_pinned"] = {"GB_per_s": e2e["GB_per_s"], "ms": e2e["ms"]}
+    for nm, v in (out.get("e2e_rows") or {}).items():
+        summ.setdefault("e2e_rows", {})[nm] = (
+            {"error": v["error"]} if "error" in v else
+            {"rows_ms": v["e2e_rows_ms"], "serial_ms": v["e2e_rows_serial_ms"],
+             "pinned_ms": v["e2e_pinned_ms"], "rows_over_pinned": v["rows_over_pinned"],
+             "bitwise": all(v["bitwise_same_as_serial"].values()),
+             "sel": (v.get("parity") or {}).get("selected_set")})
     line["summary"] = summ
     return line
 
@@ -1504,6 +1615,15 @@ def main():
 
     if rank == 0 and world == 1 and not emu and not a.no_e2e and w["dtype"] == "f64":
         out["e2e_noised_pinned"] = noised_probe(eng, dev, X, n, dl, f, m)
+
+    if rank == 0 and world == 1 and not emu and not a.no_e2e and a.workload == DEFAULT_WORKLOAD:
+        # the verifier's own input: n separate host rows
+        out["e2e_rows"] = {}
+        for nm in ("D_512x1M_f153", "B_mnist", "A_creditcard"):
+            try:
+                out["e2e_rows"][nm] = rows_entry_variant(eng, dev, nm)
+            except Exception as e:  # noqa: BLE001 -- must not cost the headline line
+                out["e2e_rows"][nm] = {"error": repr(e)}
 
     if rank == 0 and world == 1 and not emu and not a.no_cpu_baseline:
         try:

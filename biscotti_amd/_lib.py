@@ -16,7 +16,7 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
-BK_ABI_VERSION = 12
+BK_ABI_VERSION = 13
 BK_F32_EXACT, BK_F32_MFMA, BK_F32_CERTIFIED, BK_F32_I8, BK_F32_I8_CERTIFIED = 0, 1, 2, 3, 4
 BK_F32_I8X2, BK_F32_I8X2_CERTIFIED = 5, 6  # two digit planes, three products (bk.h)
 BK_F64_EXACT, BK_F64_I8, BK_F64_I8_CERTIFIED, BK_F64_I8X2, BK_F64_I8X2_CERTIFIED = 0, 3, 4, 5, 6
@@ -45,6 +45,8 @@ SIGNATURES = {
     "bk_stage_alloc": (_i, [_p, _i64, ctypes.POINTER(_p)]),
     "bk_stage_free": (_i, [_p, _p]),
     "bk_multikrum": (_i, [_p, _p, _i, _i, _i64, _i64, _i64, _i64, _p, _p, _p, _p]),
+    "bk_multikrum_rows": (_i, [_p, _p, _i, _i64, _i64, _i64, _p, _p, _p, _p]),
+    "bk_set_host_threads": (_i, [_p, _i]),
     "bk_multikrum_device": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _p, _p, _p]),
     "bk_upper_elems": (_i64, [_i64]),
     "bk_gram_upper_device": (_i, [_p, _p, _i, _i64, _i64, _i64, _p]),

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -16,6 +17,7 @@
 #include <vector>
 
 #include "../../include/bk.h"
+#include "bk_hostpool.h"
 #include "bk_internal.h"
 #include "bk_synth.h"
 
@@ -125,6 +127,14 @@ struct bk_ctx {
     hipEvent_t ev_go = nullptr, ev_cp[2] = {nullptr, nullptr}, ev_use[2] = {nullptr, nullptr};
     // host-side pinned allocations handed out by bk_stage_alloc
     std::vector<void *> staged;
+    // bk_multikrum_rows: worker threads packing the caller's separate host rows
+    // into a pinned ring (both created on first use), and the ring slots'
+    // copy-done events
+    bk::HostPool *hpool = nullptr;
+    int hthreads = 0;  // packing threads incl. the caller (bk_set_host_threads; 0: default)
+    void *rstage = nullptr;
+    size_t rstage_bytes = 0;
+    hipEvent_t ev_rows[4] = {nullptr, nullptr, nullptr, nullptr};
     // timing
     uint32_t timing = 0;  // bit k: record HIP events around kernel k (bk_timing_select)
     int tstride = 1;      // ... on every tstride-th launch of it (bk_timing_stride)
@@ -190,7 +200,10 @@ struct bk_ctx {
     // communicator (bk_create): BK_TEST_SPLIT_SCORES=R scores in R row chunks,
     // one launch each, as R ranks would (the arithmetic of the split, tested on
     // one GPU); BK_EMU_SPLIT_SCORES=R scores only rank 0's chunk once a mode's
-    // first call has scored them all (bench.py --emulate-ranks: one rank's time)
+    // first call has scored them all (bench.py --emulate-ranks: one rank's time;
+    // TIMING ONLY -- the other shares keep that first call's scores, so the
+    // outputs and the margin of later calls are not valid, and new data at the
+    // same n is not rescored)
     int64_t split_min_n = 2049;
     int test_split_scores = 0, emu_split_scores = 0;
     int test_split_fail = 0;   // BK_TEST_SPLIT_FAIL=p: under BK_TEST_SPLIT_SCORES, share p - 1 "fails"
@@ -962,6 +975,22 @@ int ensure_copy_stream(bk_ctx *c) {
     return BK_OK;
 }
 
+// The host entries' column chunk width: ~BK_STAGE_CHUNK_BYTES (default 256
+// MiB) of the batch plus its k noise vectors per chunk, a multiple of 64
+// columns (16-B aligned chunk starts), at most 64 chunks (every chunk writes
+// and adds one packed partial Gram -- n^2/2 doubles, 1 GiB at n = 16384 --
+// which must stay small against its copy).  bk_multikrum and
+// bk_multikrum_rows chunk alike, so their chunk Grams sum in the same order.
+int64_t host_chunk_cols(int64_t n, size_t es, int64_t k, int64_t d) {
+    int64_t cap = (int64_t)256 << 20;
+    if (const char *v = getenv("BK_STAGE_CHUNK_BYTES")) cap = atoll(v) > 0 ? atoll(v) : cap;
+    const int64_t col_bytes = n * (int64_t)es + n * k * (int64_t)sizeof(double);
+    int64_t W = cap / col_bytes;
+    W = W < (d + 63) / 64 ? (d + 63) / 64 : W;
+    W = W < 64 ? 64 : (W + 63) / 64 * 64;
+    return W >= d ? d : W;
+}
+
 // Host entries (bk_multikrum, bk_multikrum_noised): the batch crosses PCIe in
 // column chunks on a copy stream, and each chunk's partial Gram (K1 + K1b,
 // after K6 when noise is applied) runs on the compute stream while the next
@@ -976,17 +1005,7 @@ int stage_host_pipelined(bk_ctx *c, const void *X, int64_t ld, int dtype, const 
                          int64_t dld, double *U, Plan &pl) {
     const size_t es = esize(dtype);
     CHK(ensure_copy_stream(c));
-    // chunks of ~BK_STAGE_CHUNK_BYTES (default 256 MiB) of the batch plus its
-    // noise; widths a multiple of 64 columns (16-B aligned chunk starts)
-    int64_t cap = (int64_t)256 << 20;
-    if (const char *v = getenv("BK_STAGE_CHUNK_BYTES")) cap = atoll(v) > 0 ? atoll(v) : cap;
-    const int64_t col_bytes = n * (int64_t)es + n * k * (int64_t)sizeof(double);
-    // at most 64 chunks: every chunk writes and adds one packed partial Gram
-    // (n^2/2 doubles: 1 GiB at n = 16384), which must stay small against its copy
-    int64_t W = cap / col_bytes;
-    W = W < (d + 63) / 64 ? (d + 63) / 64 : W;
-    W = W < 64 ? 64 : (W + 63) / 64 * 64;
-    if (W >= d) W = d;
+    const int64_t W = host_chunk_cols(n, es, k, d);
     const int64_t C = (d + W - 1) / W;
     const size_t usz = (size_t)bk_upper_elems(n);
     double *P = nullptr;
@@ -1231,6 +1250,232 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
     return BK_OK;
 }
 
+// ---- the row-fed host entry (bk_multikrum_rows) ----------------------------
+// Biscotti's verifier holds the batch as n separately allocated host rows
+// (getTopKRUMIndex(deltas [][]float64), krum.go:100-166; each row a peer's
+// RPC-decoded slice).  Before anything crosses PCIe the rows must be in
+// pinned memory.  The cgo shim used to pack them serially into a pinned batch
+// (one core, 4.3 GB at config D) and only then call bk_multikrum; here the
+// packing runs on several host threads into a ring of pinned slots, and each
+// slot's H2D (and the Gram of its columns) starts as soon as it is full.
+
+// packing threads, the caller's included: bk_set_host_threads, else
+// BK_HOST_THREADS, else min(16, the host's hardware threads)
+int host_threads(const bk_ctx *c) {
+    if (c->hthreads > 0) return c->hthreads;
+    static const int def = [] {
+        if (const char *v = getenv("BK_HOST_THREADS"))
+            if (atoi(v) > 0) return std::min(atoi(v), 256);
+        const unsigned hw = std::thread::hardware_concurrency();
+        return (int)std::max(1u, std::min(16u, hw ? hw : 1u));
+    }();
+    return def;
+}
+
+// the context's worker pool (threads - 1 workers), or nullptr when the caller
+// packs alone (one thread, or the workers could not be started)
+bk::HostPool *get_pool(bk_ctx *c) {
+    const int t = host_threads(c);
+    if (c->hpool && c->hpool->workers() == t - 1) return c->hpool;
+    delete c->hpool;
+    c->hpool = nullptr;
+    if (t <= 1) return nullptr;
+    try {
+        c->hpool = new bk::HostPool(t - 1);
+    } catch (...) {
+        c->hpool = nullptr;
+    }
+    return c->hpool;
+}
+
+// one packing job on the pool for the lifetime of this object: the pool's
+// end() runs on every return path, so no worker still uses the job function
+// (on the caller's stack) or writes into the stage after the entry returns
+struct PoolJob {
+    bk::HostPool *pool;
+    PoolJob(bk::HostPool *p, int nitems, const std::function<void(int)> *fn) : pool(p) {
+        if (pool) pool->begin(nitems, fn);
+    }
+    ~PoolJob() {
+        if (pool) pool->end();
+    }
+};
+
+// the pack's stores: non-temporal (default), or plain memcpy (BK_ROWS_COPY=memcpy,
+// an A/B of the same bytes)
+bool rows_copy_nt() {
+    const char *e = getenv("BK_ROWS_COPY");
+    return !(e && strcmp(e, "memcpy") == 0);
+}
+
+// the pinned ring (grow-only; every call is synchronous, so no copy from the
+// old ring is in flight when it is replaced)
+int ensure_rows_stage(bk_ctx *c, size_t bytes) {
+    if (c->rstage_bytes >= bytes) return BK_OK;
+    if (c->rstage) (void)hipHostFree(c->rstage);
+    c->rstage = nullptr;
+    c->rstage_bytes = 0;
+    HIPCHK(hipHostMalloc(&c->rstage, bytes, hipHostMallocPortable | hipHostMallocMapped));
+    c->rstage_bytes = bytes;
+    return BK_OK;
+}
+
+int ensure_rows_events(bk_ctx *c) {
+    for (hipEvent_t &e : c->ev_rows)
+        if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return BK_OK;
+}
+
+// Column chunks of the batch through a ring of S <= 3 pinned slots: chunk ch
+// (columns [ch W, ch W + W)) is packed by the pool into slot ch mod S (row
+// blocks of ~2 MiB are the items), crosses PCIe on the copy stream into the
+// device batch dX (row stride dld), and its partial Gram runs on the compute
+// stream, as in stage_host_pipelined.  A slot is handed back to the packers
+// when its copy has landed, so the packing of chunks ch + 1 .. ch + S - 1
+// overlaps the copy of chunk ch.  The chunks are bk_multikrum's
+// (host_chunk_cols), summed in the same order: every output is bitwise that of
+// bk_multikrum on the rows packed into one pinned batch.
+int stage_rows_pipelined(bk_ctx *c, const char *const *rows, int dtype, int64_t n, int64_t d,
+                         char *dX, int64_t dld, double *U, Plan &pl) {
+    const size_t es = esize(dtype);
+    CHK(ensure_copy_stream(c));
+    CHK(ensure_rows_events(c));
+    const int64_t W = host_chunk_cols(n, es, 0, d);
+    const int64_t C = (d + W - 1) / W;
+    const int S = (int)std::min<int64_t>(C, 3);
+    const size_t slot = (size_t)n * W * es;
+    CHK(ensure_rows_stage(c, slot * S));
+    const size_t usz = (size_t)bk_upper_elems(n);
+    double *P = nullptr;
+    if (C > 1) {
+        CHK(ensure(c->Ug, usz * sizeof(double)));
+        P = (double *)c->Ug.p;
+    }
+    // items: blocks of rb rows of one chunk, ~2 MiB each
+    const int64_t rb = std::max<int64_t>(1, std::min<int64_t>(n, ((int64_t)2 << 20) / (W * (int64_t)es)));
+    const int64_t ipc = (n + rb - 1) / rb;
+    std::unique_ptr<std::atomic<int64_t>[]> done(new std::atomic<int64_t>[C]);
+    for (int64_t ch = 0; ch < C; ++ch) done[ch].store(0, std::memory_order_relaxed);
+    char *stage = (char *)c->rstage;
+    const bool nt = rows_copy_nt();
+    const std::function<void(int)> fn = [&](int it) {
+        const int64_t ch = it / ipc, r0 = (it % ipc) * rb, r1 = std::min(n, r0 + rb);
+        const int64_t c0 = ch * W, wc = std::min(W, d - c0);
+        char *sl = stage + (size_t)(ch % S) * slot;
+        for (int64_t r = r0; r < r1; ++r)
+            bk::copy_to_stage(sl + (size_t)r * wc * es, rows[r] + (size_t)c0 * es, (size_t)wc * es,
+                              nt);
+        _mm_sfence();
+        done[ch].fetch_add(1, std::memory_order_release);
+    };
+    // on an error return, copies already queued may still read the stage and
+    // write dX: drain both streams (after the pool has stopped, below)
+    HostDrain drain{c};
+    // earlier work on the compute stream may still read the device batch
+    HIPCHK(hipEventRecord(c->ev_go, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->copy, c->ev_go, 0));
+    bk::HostPool *pool = get_pool(c);
+    PoolJob job(pool, (int)(C * ipc), &fn);
+    if (pool) pool->release((int)(S * ipc));
+    for (int64_t ch = 0; ch < C; ++ch) {
+        const int64_t c0 = ch * W, wc = std::min(W, d - c0);
+        const int s = (int)(ch % S);
+        if (pool) {
+            while (done[ch].load(std::memory_order_acquire) < ipc)
+                if (!pool->help()) _mm_pause();
+        } else {
+            for (int64_t i = ch * ipc; i < (ch + 1) * ipc; ++i) fn((int)i);
+        }
+        HIPCHK(hipMemcpy2DAsync(dX + c0 * es, (size_t)dld * es, stage + (size_t)s * slot,
+                                (size_t)wc * es, (size_t)wc * es, (size_t)n, hipMemcpyHostToDevice,
+                                c->copy));
+        HIPCHK(hipEventRecord(c->ev_rows[s], c->copy));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_rows[s], 0));
+        CHK(stage_gram(c, dX + c0 * es, dtype, n, wc, dld, ch == 0 ? U : P, pl));
+        if (ch > 0) HIPCHK(launch_add_upper(U, P, (int64_t)usz, c->stream));
+        // chunk ch - 1's slot is free once its copy (queued before chunk ch's,
+        // which keeps the copy engine busy meanwhile) has landed: chunk
+        // ch - 1 + S goes into it
+        if (ch >= 1 && ch - 1 + S < C) {
+            HIPCHK(hipEventSynchronize(c->ev_rows[(ch - 1) % S]));
+            if (pool) pool->release((int)((ch + S) * ipc));
+        }
+    }
+    pl.d = d;
+    drain.armed = false;
+    return BK_OK;
+}
+
+// Biscotti's deployed shapes (n <= 128, d <= 32768: configs A and B) on the
+// row-fed entry.  k_tiny's batches (n <= 16, d <= 128) are packed by the
+// caller into the mapped pinned stage, which the kernel reads over PCIe (as
+// bk_multikrum's pinned batches).  Larger ones are packed by the pool in
+// row order into a stage laid out like the device batch (16-B rows), and
+// each group of rows crosses PCIe as one linear copy on the compute stream
+// as soon as it is packed (BK_ROWS_GROUPS groups, default 4), so the copy
+// engine starts after the first ~quarter of the pack instead of after all
+// of it; then the one-launch k_small, as bk_multikrum's host path.
+int run_rows_small(bk_ctx *c, const char *const *rows, int dtype, int64_t n, int64_t d, int64_t f,
+                   int64_t *sel_idx, int64_t *m_out, double *scores, double *mean_out) {
+    const size_t es = esize(dtype);
+    const int64_t epg = (int64_t)(16 / es);
+    const int64_t dld = (d + epg - 1) / epg * epg;
+    const size_t rowb = (size_t)dld * es;
+    CHK(ensure_rows_stage(c, (size_t)n * rowb));
+    char *stage = (char *)c->rstage;
+    if (tiny_ok((int)n, d)) {
+        for (int64_t r = 0; r < n; ++r) memcpy(stage + (size_t)r * rowb, rows[r], (size_t)d * es);
+        return run_host_small(c, stage, BK_HOST_PINNED, dld, dtype, nullptr, 0, 0, n, d, f, sel_idx,
+                              m_out, scores, mean_out, nullptr, 0);
+    }
+    const char *ge = getenv("BK_ROWS_GROUPS");
+    const int groups_env = ge && atoi(ge) > 0 ? atoi(ge) : 4;
+    CHK(ensure(c->X, (size_t)n * rowb));
+    // items: ~256 KiB of rows each; group g = items [g I / G, (g + 1) I / G)
+    const int64_t ri = std::max<int64_t>(1, ((int64_t)256 << 10) / (d * (int64_t)es));
+    const int64_t I = (n + ri - 1) / ri;
+    const int64_t G = std::min<int64_t>(groups_env, I);
+    std::vector<int64_t> gstart((size_t)G + 1);
+    for (int64_t g = 0; g <= G; ++g) gstart[(size_t)g] = g * I / G;
+    std::unique_ptr<std::atomic<int64_t>[]> done(new std::atomic<int64_t>[G]);
+    for (int64_t g = 0; g < G; ++g) done[g].store(0, std::memory_order_relaxed);
+    const bool nt = rows_copy_nt();
+    const std::function<void(int)> fn = [&](int it) {
+        const int64_t r0 = it * ri, r1 = std::min(n, r0 + ri);
+        for (int64_t r = r0; r < r1; ++r)
+            bk::copy_to_stage(stage + (size_t)r * rowb, rows[r], (size_t)d * es, nt);
+        _mm_sfence();
+        int64_t g = 0;
+        while (gstart[(size_t)g + 1] <= it) ++g;
+        done[g].fetch_add(1, std::memory_order_release);
+    };
+    HostDrain drain{c};
+    {
+        bk::HostPool *pool = get_pool(c);
+        PoolJob job(pool, (int)I, &fn);
+        if (pool) pool->release((int)I);
+        char *dx = (char *)c->X.p;
+        for (int64_t g = 0; g < G; ++g) {
+            const int64_t need = gstart[(size_t)g + 1] - gstart[(size_t)g];
+            if (pool) {
+                while (done[g].load(std::memory_order_acquire) < need)
+                    if (!pool->help()) _mm_pause();
+            } else {
+                for (int64_t i = gstart[(size_t)g]; i < gstart[(size_t)g + 1]; ++i) fn((int)i);
+            }
+            const int64_t r0 = gstart[(size_t)g] * ri, r1 = std::min(n, gstart[(size_t)g + 1] * ri);
+            CHK(timed(c, BK_K_H2D, [&] {
+                return hipMemcpyAsync(dx + (size_t)r0 * rowb, stage + (size_t)r0 * rowb,
+                                      (size_t)(r1 - r0) * rowb, hipMemcpyHostToDevice, c->stream);
+            }));
+        }
+    }
+    const int st = run_host_small(c, c->X.p, BK_DEVICE, dld, dtype, nullptr, 0, 0, n, d, f, sel_idx,
+                                  m_out, scores, mean_out, nullptr, 0);
+    drain.armed = st != BK_OK;
+    return st;
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -1262,8 +1507,33 @@ int run_certified(bk_ctx *c, F &&run) {
     // only a near tie of a call whose Gram ran on the fp32 MFMA (u_G > 2^-53)
     // is re-run: an exact first pass (k_small, n <= 128) would repeat itself
     if (mg[2] == 0.0 || !(mg[8] > 0x1p-53)) return BK_OK;
+    // (BK_EMU_SPLIT_SCORES, timing only: the exact re-run's Gram is another
+    // one, so its first call scores every share again, and so does the next
+    // approximate call -- ADVICE r5)
+    c->emu_split_n = -1;
     c->force_exact = 1;
     const int st = run();
+    c->force_exact = 0;
+    c->emu_split_n = -1;
+    if (st == BK_OK) ++c->certified_reruns;
+    return st;
+}
+
+// the host entries' certified modes: a near tie of an approximate Gram re-runs
+// exact from the device-resident batch dX (row stride dld), whose outputs
+// replace the first run's in the caller's arrays
+int host_certified_rerun(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t dld,
+                         int64_t f, double *U, int64_t *sel_idx, int64_t *m_out, double *scores,
+                         double *mean_out) {
+    if (!certified(c, dtype)) return BK_OK;
+    double mg[MARGIN_WORDS];
+    CHK(read_margin(c, mg));
+    if (!(mg[2] != 0.0 && mg[8] > 0x1p-53)) return BK_OK;
+    c->force_exact = 1;
+    Plan pl2;
+    int st = stage_gram(c, dX, dtype, n, d, dld, U, pl2);
+    if (st == BK_OK)
+        st = run_host_outputs(c, dX, dtype, n, d, dld, f, U, pl2, sel_idx, m_out, scores, mean_out);
     c->force_exact = 0;
     if (st == BK_OK) ++c->certified_reruns;
     return st;
@@ -1371,8 +1641,11 @@ void bk_destroy(bk_ctx *c) {
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         for (DevBuf *b : bufs)
             if (b->p) (void)hipFree(b->p);
-        for (hipEvent_t ev : {c->ev_go, c->ev_cp[0], c->ev_cp[1], c->ev_use[0], c->ev_use[1]})
+        for (hipEvent_t ev : {c->ev_go, c->ev_cp[0], c->ev_cp[1], c->ev_use[0], c->ev_use[1],
+                              c->ev_rows[0], c->ev_rows[1], c->ev_rows[2], c->ev_rows[3]})
             if (ev) (void)hipEventDestroy(ev);
+        if (c->rstage) (void)hipHostFree(c->rstage);
+        delete c->hpool;
         if (c->copy) (void)hipStreamDestroy(c->copy);
         for (void *p : c->staged) (void)hipHostFree(p);
         for (auto &ev : c->pending) {
@@ -1607,21 +1880,39 @@ int bk_multikrum(bk_ctx *c, const void *X, int where, int dtype, int64_t n, int6
         CHK(stage_gram(c, dX, dtype, n, d, dld, U, pl));
     }
     CHK(run_host_outputs(c, dX, dtype, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out));
-    if (certified(c, dtype)) {  // exact re-run of a near tie from the device-resident batch
-        double mg[MARGIN_WORDS];
-        CHK(read_margin(c, mg));
-        if (mg[2] != 0.0 && mg[8] > 0x1p-53) {
-            c->force_exact = 1;
-            Plan pl2;
-            int st = stage_gram(c, dX, dtype, n, d, dld, U, pl2);
-            if (st == BK_OK)
-                st = run_host_outputs(c, dX, dtype, n, d, dld, f, U, pl2, sel_idx, m_out, scores,
-                                      mean_out);
-            c->force_exact = 0;
-            if (st == BK_OK) ++c->certified_reruns;
-            return st;
-        }
-    }
+    return host_certified_rerun(c, dX, dtype, n, d, dld, f, U, sel_idx, m_out, scores, mean_out);
+}
+
+int bk_multikrum_rows(bk_ctx *c, const void *const *rows, int dtype, int64_t n, int64_t d,
+                      int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
+                      double *mean_out) {
+    CHK(check_common(c, rows, dtype, n, d, d));
+    CHK(bk_check_args(n, d, f));
+    if (!sel_idx) return fail(BK_EINVAL, "null sel_idx");
+    for (int64_t i = 0; i < n; ++i)
+        if (!rows[i]) return fail(BK_EINVAL, "null row %lld", (long long)i);
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    const char *const *R = (const char *const *)rows;
+    if (small_ok(c, nullptr, dtype, n, d, d))
+        return run_rows_small(c, R, dtype, n, d, f, sel_idx, m_out, scores, mean_out);
+    const size_t es = esize(dtype);
+    const int64_t epg = (int64_t)(16 / es);
+    const int64_t dld = (d + epg - 1) / epg * epg;
+    CHK(ensure(c->X, (size_t)n * dld * es));
+    CHK(ensure(c->U, (size_t)bk_upper_elems(n) * sizeof(double)));
+    double *U = (double *)c->U.p;
+    Plan pl;
+    CHK(stage_rows_pipelined(c, R, dtype, n, d, (char *)c->X.p, dld, U, pl));
+    CHK(run_host_outputs(c, c->X.p, dtype, n, d, dld, f, U, pl, sel_idx, m_out, scores, mean_out));
+    return host_certified_rerun(c, c->X.p, dtype, n, d, dld, f, U, sel_idx, m_out, scores, mean_out);
+}
+
+int bk_set_host_threads(bk_ctx *c, int threads) {
+    if (!c) return fail(BK_EINVAL, "null context");
+    if (threads < 0 || threads > 256) return fail(BK_EINVAL, "threads=%d out of [0, 256]", threads);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->hthreads = threads;
     return BK_OK;
 }
 

@@ -152,6 +152,55 @@ class Engine:
         assert mo.value == m
         return sel, sc, mean
 
+    # ---- row-fed host entry (bk_multikrum_rows): n separate host rows, ---
+    #      as the Go verifier holds them (deltas [][]float64, krum.go:100-166)
+    def multikrum_rows(self, rows, f, want_scores=True, want_mean=True):
+        """rows: a sequence of n 1-D arrays (all float64 or all float32, each d
+        long, each contiguous); they are packed on libbk's host threads, not
+        here.  Returns (sel, scores, mean) as multikrum."""
+        rows = list(rows)
+        n = len(rows)
+        if n == 0:
+            raise ValueError("no rows")
+        dt = np.asarray(rows[0]).dtype
+        if dt not in (np.float64, np.float32):
+            raise ValueError("rows must be float64 or float32")
+        keep = []
+        for r in rows:
+            a = np.asarray(r)
+            if a.dtype != dt or a.ndim != 1:
+                raise ValueError("every row must be a 1-D array of the first row's dtype")
+            keep.append(a if a.flags.c_contiguous else np.ascontiguousarray(a))
+        d = keep[0].shape[0]
+        if any(a.shape[0] != d for a in keep):
+            raise ValueError("ragged rows")
+        f = int(f)
+        check(lib().bk_check_args(n, d, f))
+        m = n - f
+        ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in keep])
+        sel = np.empty(m, dtype=np.int64)
+        mo = ctypes.c_int64(0)
+        sc = np.empty(n, dtype=np.float64) if want_scores else None
+        mean = np.empty(d, dtype=np.float64) if want_mean else None
+        check(lib().bk_multikrum_rows(self._ctx, ptrs, _lib.BK_F32 if dt == np.float32 else
+                                      _lib.BK_F64, n, d, f, sel.ctypes.data,
+                                      ctypes.addressof(mo),
+                                      sc.ctypes.data if sc is not None else None,
+                                      mean.ctypes.data if mean is not None else None))
+        assert mo.value == m
+        return sel, sc, mean
+
+    def multikrum_rows_ptr(self, row_ptrs, dtype, n, d, f, sel_ptr, scores_ptr=None,
+                           mean_ptr=None):
+        """Raw host row pointers (a ctypes c_void_p array); host outputs."""
+        mo = ctypes.c_int64(0)
+        check(lib().bk_multikrum_rows(self._ctx, row_ptrs, dtype, n, d, f, _p(sel_ptr),
+                                      ctypes.addressof(mo), _p(scores_ptr), _p(mean_ptr)))
+        return mo.value
+
+    def set_host_threads(self, threads):
+        check(lib().bk_set_host_threads(self._ctx, int(threads)))
+
     # ---- host entry with the noise applied in the H2D staging -----------
     #      (bk_multikrum_noised, SURVEY.md §8(f) row 3) -------------------
     def multikrum_noised(self, delta, noise, f, want_scores=True, want_mean=True,
@@ -461,7 +510,11 @@ class KRUMValidator:
         clip = int(self.NumAdversaries * float(n))
         if self._engine is None:
             self.initialize()
-        return [int(i) for i in krum(np.asarray(deltas, dtype=np.float64), clip, self._engine)]
+        # the rows go to libbk as they are (bk_multikrum_rows: packed on its
+        # host threads into pinned memory, as the cgo shim hands Go's slices)
+        rows = [np.asarray(r, dtype=np.float64) for r in deltas]
+        sel, _, _ = self._engine.multikrum_rows(rows, clip, want_scores=False, want_mean=False)
+        return [int(i) for i in sel]
 
     def flush_collected_updates(self, collecting_updates=False):
         # krum.go:169-176

@@ -29,6 +29,7 @@ import "C"
 
 import (
 	"os"
+	"runtime"
 	"strconv"
 	"unsafe"
 )
@@ -73,6 +74,14 @@ func (krumval *KRUMValidator) initialize() {
 // reference returned numpy argpartition order, and its only consumer,
 // checkIfAccepted, tests membership.  On any engine error every update is
 // rejected (empty list), which is what a failing Python call led to.
+//
+// The rows go to libbk as they are (bk_multikrum_rows): a C array of the n
+// row pointers, each row's backing array pinned for the call -- Go pointers
+// stored in C memory, legal while pinned (runtime.Pinner, Go >= 1.21).  libbk
+// packs them into its own pinned memory on host threads, each column chunk's
+// H2D and Gram starting as soon as it is packed, instead of this goroutine
+// copying all n rows into a pinned batch first (the old serial pack, kept
+// for the multi-GPU group below).
 func (krumval *KRUMValidator) getTopKRUMIndex(deltas [][]float64) []int {
 	n := len(deltas)
 	if n == 0 || bkCtx == nil {
@@ -84,38 +93,30 @@ func (krumval *KRUMValidator) getTopKRUMIndex(deltas [][]float64) []int {
 		outLog.Printf("Krum: %s", C.GoString(C.bk_last_error()))
 		return []int{}
 	}
-	need := int64(n) * int64(d) * 8
-	if need > bkStageLen {
-		if bkStage != nil {
-			C.bk_stage_free(bkCtx, bkStage)
-		}
-		var p unsafe.Pointer
-		if C.bk_stage_alloc(bkCtx, C.int64_t(need), &p) != C.BK_OK {
-			outLog.Printf("Krum: %s", C.GoString(C.bk_last_error()))
-			bkStage, bkStageLen = nil, 0
-			return []int{}
-		}
-		bkStage, bkStageLen = p, need
-	}
-	// pack [][]float64 rows into the pinned C buffer (row-major n x d)
-	stage := unsafe.Slice((*float64)(bkStage), n*d)
 	for i := 0; i < n; i++ {
 		if len(deltas[i]) != d {
 			outLog.Printf("Krum: ragged update %d (%d != %d)", i, len(deltas[i]), d)
 			return []int{}
 		}
-		copy(stage[i*d:(i+1)*d], deltas[i])
 	}
 	m := n - f
 	sel := make([]C.int64_t, m)
 	var mOut C.int64_t
 	var st C.int
 	if bkGroup != nil {
-		st = C.bk_group_multikrum(bkGroup, bkStage, C.BK_HOST_PINNED, C.BK_F64, C.int64_t(n),
-			C.int64_t(d), C.int64_t(d), C.int64_t(f), (*C.int64_t)(unsafe.Pointer(&sel[0])), &mOut,
-			nil, nil)
+		st = groupTopKRUM(deltas, n, d, f, sel, &mOut)
 	} else {
-		st = C.bk_multikrum(bkCtx, bkStage, C.BK_HOST_PINNED, C.BK_F64, C.int64_t(n), C.int64_t(d),
+		var pinner runtime.Pinner
+		defer pinner.Unpin()
+		var rowsC unsafe.Pointer
+		rowsC = C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0))))
+		defer C.free(rowsC)
+		ptrs := unsafe.Slice((*unsafe.Pointer)(rowsC), n)
+		for i := 0; i < n; i++ {
+			pinner.Pin(&deltas[i][0])
+			ptrs[i] = unsafe.Pointer(&deltas[i][0])
+		}
+		st = C.bk_multikrum_rows(bkCtx, (*unsafe.Pointer)(rowsC), C.BK_F64, C.int64_t(n),
 			C.int64_t(d), C.int64_t(f), (*C.int64_t)(unsafe.Pointer(&sel[0])), &mOut, nil, nil)
 	}
 	if st != C.BK_OK {
@@ -128,6 +129,32 @@ func (krumval *KRUMValidator) getTopKRUMIndex(deltas [][]float64) []int {
 		out[i] = int(sel[i])
 	}
 	return out
+}
+
+// groupTopKRUM: BK_GPUS > 1 -- the rows packed into the C-owned pinned batch
+// (serially, on this goroutine), then bk_group_multikrum, each GPU copying its
+// column shard over its own PCIe link.
+func groupTopKRUM(deltas [][]float64, n, d, f int, sel []C.int64_t, mOut *C.int64_t) C.int {
+	need := int64(n) * int64(d) * 8
+	if need > bkStageLen {
+		if bkStage != nil {
+			C.bk_stage_free(bkCtx, bkStage)
+		}
+		var p unsafe.Pointer
+		if st := C.bk_stage_alloc(bkCtx, C.int64_t(need), &p); st != C.BK_OK {
+			bkStage, bkStageLen = nil, 0
+			return st
+		}
+		bkStage, bkStageLen = p, need
+	}
+	// pack [][]float64 rows into the pinned C buffer (row-major n x d)
+	stage := unsafe.Slice((*float64)(bkStage), n*d)
+	for i := 0; i < n; i++ {
+		copy(stage[i*d:(i+1)*d], deltas[i])
+	}
+	return C.bk_group_multikrum(bkGroup, bkStage, C.BK_HOST_PINNED, C.BK_F64, C.int64_t(n),
+		C.int64_t(d), C.int64_t(d), C.int64_t(f), (*C.int64_t)(unsafe.Pointer(&sel[0])), mOut,
+		nil, nil)
 }
 
 // getTopKRUMIndexNoised is the same verifier call for updates that carry Delta

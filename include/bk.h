@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 12
+#define BK_ABI_VERSION 13
 
 typedef struct bk_ctx bk_ctx;
 
@@ -102,6 +102,29 @@ int bk_stage_free(bk_ctx *ctx, void *pinned);
 int bk_multikrum(bk_ctx *ctx, const void *X, int where, int dtype, int64_t n, int64_t d,
                  int64_t ld, int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
                  double *mean_out);
+
+/* The verifier's own input: n SEPARATE host rows (getTopKRUMIndex(deltas
+ * [][]float64), krum.go:100-166 -- one slice per peer, as RPC decoded them,
+ * replacing the shim's serial pack of the rows into a pinned batch,
+ * krum.go:117-125's marshalling loop in the reference).  rows[i] points at
+ * update i's d elements (dtype; pageable or pinned host memory, any
+ * alignment); the rows are only read, during the call.  libbk packs them on
+ * host threads (bk_set_host_threads) into a ring of C-owned pinned slots,
+ * column chunk by column chunk, and each chunk's H2D and partial Gram start
+ * as soon as it is packed.  Outputs and contract as bk_multikrum (host
+ * outputs, synchronous); the selection and the mean are bitwise those of
+ * bk_multikrum(BK_HOST_PINNED) on the same rows packed row-major.
+ * cgo: the row pointers are Go pointers stored in C memory, which Go >= 1.21
+ * allows while each row's backing array is pinned (runtime.Pinner) for the
+ * call (go/bk/krum_bk.go).  A null row is BK_EINVAL. */
+int bk_multikrum_rows(bk_ctx *ctx, const void *const *rows, int dtype, int64_t n, int64_t d,
+                      int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
+                      double *mean_out);
+/* Host threads that pack bk_multikrum_rows' rows, the caller's included (1:
+ * the caller alone; 0: the default, BK_HOST_THREADS or min(16, hardware
+ * threads)).  The workers are started on the next call and sleep between
+ * calls. */
+int bk_set_host_threads(bk_ctx *ctx, int threads);
 
 /* Device-resident, asynchronous on the context stream.  All pointers are
  * device pointers; d_sel_idx gets m = n-f ascending indices; d_scores (n) and

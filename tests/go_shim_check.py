@@ -129,9 +129,9 @@ def _go_type_to_c(t, name):
 
 
 def _functions(go_text):
-    """(name, body) of each top-level func."""
+    """(name, parameter list, body) of each top-level func."""
     out = []
-    for mt in re.finditer(r"^func\s+(?:\([^)]*\)\s*)?(\w+)\([^)]*\)[^{]*\{", go_text, re.M):
+    for mt in re.finditer(r"^func\s+(?:\([^)]*\)\s*)?(\w+)\(([^)]*)\)[^{]*\{", go_text, re.M):
         depth, i = 0, mt.end() - 1
         for j in range(i, len(go_text)):
             if go_text[j] == "{":
@@ -139,9 +139,26 @@ def _functions(go_text):
             elif go_text[j] == "}":
                 depth -= 1
                 if depth == 0:
-                    out.append((mt.group(1), go_text[i + 1:j]))
+                    out.append((mt.group(1), mt.group(2), go_text[i + 1:j]))
                     break
     return out
+
+
+def _param_decls(params):
+    """Go parameters ("n, d, f int, sel []C.int64_t, mOut *C.int64_t") ->
+    {name: C declaration} for the types _go_type_to_c maps."""
+    d, pending = {}, []
+    for p in [x.strip() for x in params.split(",") if x.strip()]:
+        parts = p.split(None, 1)
+        pending.append(parts[0])
+        if len(parts) == 2:  # a type closes the names collected so far
+            for nm in pending:
+                try:
+                    d[nm] = _go_type_to_c(parts[1], nm)
+                except ValueError:
+                    pass
+            pending = []
+    return d
 
 
 def _decls(text):
@@ -160,6 +177,9 @@ def _decls(text):
 
 def _to_c(expr):
     e = expr
+    # (*unsafe.Pointer)(p): cgo's Go view of a `const void *const *` (or `void **`)
+    # parameter -- cgo drops the qualifiers, so the C view is the prototype's
+    e = re.sub(r"\(\*unsafe\.Pointer\)", "(const void *const *)", e)
     e = re.sub(r"\(\*C\.(\w+)\)", r"(\1 *)", e)                              # (*C.T)(p)
     e = re.sub(r"\bC\.(int64_t|int32_t|int|double|size_t|uint32_t)\(", r"(\1)(", e)  # C.int64_t(x)
     e = re.sub(r"\bunsafe\.Pointer\(", "(void *)(", e)
@@ -178,12 +198,12 @@ def shim_as_c(go_text):
     lines = ["#include <stddef.h>", "#include <stdint.h>", '#include "bk.h"', ""]
     for nm, decl in pkg.items():
         lines.append("static %s;" % decl)
-    for fname, body in _functions(go_text):
+    for fname, params, body in _functions(go_text):
         calls = [(m.group(1), _call_args(body, m.end() - 1))
                  for m in re.finditer(r"\bC\.(bk_\w+)\s*\(", body)]
         if not calls:
             continue
-        loc = _decls(body)
+        loc = dict(_param_decls(params), **_decls(body))
         used = set()
         for _, a in calls:
             used |= set(re.findall(r"(?<![\w.])([A-Za-z_]\w*)\b(?!\s*\()", _to_c(a)))
@@ -192,7 +212,7 @@ def shim_as_c(go_text):
             if nm in loc:
                 lines.append("    %s;" % loc[nm])
             elif nm in pkg or nm.startswith("BK_") or nm == "NULL" or re.match(
-                    r"^(int64_t|int32_t|int|double|void|size_t|uint32_t|bk_\w+)$", nm):
+                    r"^(int64_t|int32_t|int|double|void|const|size_t|uint32_t|bk_\w+)$", nm):
                 continue
             else:  # a Go int local (n, d, f, k, need, g, m ...)
                 lines.append("    long long %s = 1;" % nm)

@@ -43,7 +43,8 @@ def _proto_span(text, name):
 
 def test_shim_uses_the_abi_entries():
     # the drop-in's own entry points must be among them
-    for name in ("bk_create", "bk_multikrum", "bk_stage_alloc", "bk_last_error",
+    # (r6: the verifier's rows go through bk_multikrum_rows -- VERDICT r5 item 1)
+    for name in ("bk_create", "bk_multikrum_rows", "bk_stage_alloc", "bk_last_error",
                  "bk_selection_margin", "bk_multikrum_noised", "bk_group_multikrum"):
         assert name in USED, name
     assert {"BK_OK", "BK_HOST_PINNED", "BK_F64"} <= set(CONSTS)
@@ -89,14 +90,19 @@ def test_adding_a_parameter_fails(tmp_path, name):
     assert not ok
 
 
-def test_a_pointer_parameter_changing_type_fails(tmp_path):
-    """bk_multikrum's sel_idx as int32_t*: the shim's (*C.int64_t) no longer fits."""
-    s, op, cp = _proto_span(HDR, "bk_multikrum")
-    proto = HDR[op:cp].replace("int64_t *sel_idx", "int32_t *sel_idx")
+@pytest.mark.parametrize("name,old,new", [
+    # sel_idx as int32_t*: the shim's (*C.int64_t) no longer fits
+    ("bk_multikrum_rows", "int64_t *sel_idx", "int32_t *sel_idx"),
+    ("bk_multikrum_noised", "int64_t *sel_idx", "int32_t *sel_idx"),
+    # the row-pointer array as a flat batch: the shim's (*unsafe.Pointer) no longer fits
+    ("bk_multikrum_rows", "const void *const *rows", "const double *rows")])
+def test_a_pointer_parameter_changing_type_fails(tmp_path, name, old, new):
+    s, op, cp = _proto_span(HDR, name)
+    proto = HDR[op:cp].replace(old, new)
     assert proto != HDR[op:cp]
     bad = HDR[:op] + proto + HDR[cp:]
     ok, err, _ = G.compile_check(GO, _write_header(tmp_path, bad))
-    assert not ok and "bk_multikrum" in err
+    assert not ok and name in err
 
 
 @pytest.mark.parametrize("const", CONSTS)

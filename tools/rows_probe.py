@@ -1,0 +1,44 @@
+"""Probe of the row-fed host entry (bk_multikrum_rows) on one GPU: bench.py's
+rows_entry_variant at the given configs, one JSON object per config.
+
+    python tools/rows_probe.py [D_512x1M_f153 B_mnist A_creditcard]
+    python tools/rows_probe.py --sweep B_mnist   # groups x copy kind x threads
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+    from biscotti_amd.krum import Engine
+    args = sys.argv[1:]
+    sweep = "--sweep" in args
+    names = [a for a in args if not a.startswith("--")] or ["D_512x1M_f153", "B_mnist",
+                                                            "A_creditcard"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    eng = Engine(0)
+    for nm in names:
+        if not sweep:
+            print(json.dumps({nm: bench.rows_entry_variant(eng, dev, nm)}), flush=True)
+            continue
+        for kind in ("nt", "memcpy"):
+            os.environ["BK_ROWS_COPY"] = kind
+            for g in ("1", "2", "4", "8"):
+                os.environ["BK_ROWS_GROUPS"] = g
+                r = bench.rows_entry_variant(eng, dev, nm, thread_sweep=(1, 2, 4, 8, 16))
+                print(json.dumps({"name": nm, "copy": kind, "groups": g,
+                                  "rows_ms": r["e2e_rows_ms"], "pinned_ms": r["e2e_pinned_ms"],
+                                  "serial_ms": r["e2e_rows_serial_ms"],
+                                  "by_threads": r["e2e_rows_ms_by_threads"],
+                                  "bitwise": r["bitwise_same_as_serial"]}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
