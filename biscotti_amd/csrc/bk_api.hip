@@ -1260,14 +1260,16 @@ int run_host_small(bk_ctx *c, const void *X, int where, int64_t ld, int dtype, c
 // slot's H2D (and the Gram of its columns) starts as soon as it is full.
 
 // packing threads, the caller's included: bk_set_host_threads, else
-// BK_HOST_THREADS, else min(16, the host's hardware threads)
+// BK_HOST_THREADS, else min(8, the host's hardware threads) -- config D's
+// pack keeps ahead of PCIe from 4 threads on (78-79 ms per call at 4, 8 and
+// 16), and more threads only compete for the process's CPU share
 int host_threads(const bk_ctx *c) {
     if (c->hthreads > 0) return c->hthreads;
     static const int def = [] {
         if (const char *v = getenv("BK_HOST_THREADS"))
             if (atoi(v) > 0) return std::min(atoi(v), 256);
         const unsigned hw = std::thread::hardware_concurrency();
-        return (int)std::max(1u, std::min(16u, hw ? hw : 1u));
+        return (int)std::max(1u, std::min(8u, hw ? hw : 1u));
     }();
     return def;
 }
@@ -1301,11 +1303,16 @@ struct PoolJob {
     }
 };
 
-// the pack's stores: non-temporal (default), or plain memcpy (BK_ROWS_COPY=memcpy,
-// an A/B of the same bytes)
-bool rows_copy_nt() {
+// the pack's stores: non-temporal for the column-chunk ring (GBs streamed
+// through it: the stores bypass the caches), cached memcpy for the small
+// path's stage (<= 32 MiB, re-used every call: it stays in the L3, and r6's
+// sweep at config B gave ~0.195 ms per call against ~0.205 non-temporal);
+// BK_ROWS_COPY=nt|memcpy forces one (an A/B of the same bytes)
+bool rows_copy_nt(bool dflt) {
     const char *e = getenv("BK_ROWS_COPY");
-    return !(e && strcmp(e, "memcpy") == 0);
+    if (e && strcmp(e, "memcpy") == 0) return false;
+    if (e && strcmp(e, "nt") == 0) return true;
+    return dflt;
 }
 
 // the pinned ring (grow-only; every call is synchronous, so no copy from the
@@ -1357,7 +1364,7 @@ int stage_rows_pipelined(bk_ctx *c, const char *const *rows, int dtype, int64_t 
     std::unique_ptr<std::atomic<int64_t>[]> done(new std::atomic<int64_t>[C]);
     for (int64_t ch = 0; ch < C; ++ch) done[ch].store(0, std::memory_order_relaxed);
     char *stage = (char *)c->rstage;
-    const bool nt = rows_copy_nt();
+    const bool nt = rows_copy_nt(true);
     const std::function<void(int)> fn = [&](int it) {
         const int64_t ch = it / ipc, r0 = (it % ipc) * rb, r1 = std::min(n, r0 + rb);
         const int64_t c0 = ch * W, wc = std::min(W, d - c0);
@@ -1412,9 +1419,11 @@ int stage_rows_pipelined(bk_ctx *c, const char *const *rows, int dtype, int64_t 
 // bk_multikrum's pinned batches).  Larger ones are packed by the pool in
 // row order into a stage laid out like the device batch (16-B rows), and
 // each group of rows crosses PCIe as one linear copy on the compute stream
-// as soon as it is packed (BK_ROWS_GROUPS groups, default 4), so the copy
-// engine starts after the first ~quarter of the pack instead of after all
-// of it; then the one-launch k_small, as bk_multikrum's host path.
+// as soon as it is packed (BK_ROWS_GROUPS groups, default 3, growing x1.5),
+// so the copy engine starts after the first sixth of the pack instead of
+// after all of it; then the one-launch k_small, as bk_multikrum's host path.
+// (r6 sweep at config B, tools/rows_probe.py --sweep: every extra copy costs
+// more than the pack it hides beyond 3-4 groups.)
 int run_rows_small(bk_ctx *c, const char *const *rows, int dtype, int64_t n, int64_t d, int64_t f,
                    int64_t *sel_idx, int64_t *m_out, double *scores, double *mean_out) {
     const size_t es = esize(dtype);
@@ -1429,17 +1438,32 @@ int run_rows_small(bk_ctx *c, const char *const *rows, int dtype, int64_t n, int
                               m_out, scores, mean_out, nullptr, 0);
     }
     const char *ge = getenv("BK_ROWS_GROUPS");
-    const int groups_env = ge && atoi(ge) > 0 ? atoi(ge) : 4;
+    const int groups_env = ge && atoi(ge) > 0 ? atoi(ge) : 3;
     CHK(ensure(c->X, (size_t)n * rowb));
-    // items: ~256 KiB of rows each; group g = items [g I / G, (g + 1) I / G)
-    const int64_t ri = std::max<int64_t>(1, ((int64_t)256 << 10) / (d * (int64_t)es));
+    // items: ~128 KiB of rows each.  Groups grow geometrically (x1.5): the
+    // copy engine starts after the first small group is packed, and each
+    // later group is packed (by several threads, faster than PCIe drains
+    // the stage) while the groups before it are in flight
+    const int64_t ri = std::max<int64_t>(1, ((int64_t)128 << 10) / (d * (int64_t)es));
     const int64_t I = (n + ri - 1) / ri;
     const int64_t G = std::min<int64_t>(groups_env, I);
     std::vector<int64_t> gstart((size_t)G + 1);
-    for (int64_t g = 0; g <= G; ++g) gstart[(size_t)g] = g * I / G;
+    {
+        double tot = 0, w = 1;
+        for (int64_t g = 0; g < G; ++g, w *= 1.5) tot += w;
+        double acc = 0;
+        w = 1;
+        gstart[0] = 0;
+        for (int64_t g = 1; g <= G; ++g, w *= 1.5) {
+            acc += w;
+            gstart[(size_t)g] = std::max(gstart[(size_t)g - 1] + 1,
+                                         std::min<int64_t>(I - (G - g), (int64_t)(I * acc / tot + 0.5)));
+        }
+        gstart[(size_t)G] = I;
+    }
     std::unique_ptr<std::atomic<int64_t>[]> done(new std::atomic<int64_t>[G]);
     for (int64_t g = 0; g < G; ++g) done[g].store(0, std::memory_order_relaxed);
-    const bool nt = rows_copy_nt();
+    const bool nt = rows_copy_nt(false);
     const std::function<void(int)> fn = [&](int it) {
         const int64_t r0 = it * ri, r1 = std::min(n, r0 + ri);
         for (int64_t r = r0; r < r1; ++r)
@@ -1450,10 +1474,19 @@ int run_rows_small(bk_ctx *c, const char *const *rows, int dtype, int64_t n, int
         done[g].fetch_add(1, std::memory_order_release);
     };
     HostDrain drain{c};
+    // debug (probe build): host timeline of the call, us from entry
+    const bool trace = probe_env("BK_ROWS_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> tl;
+    auto mark = [&] {
+        if (trace)
+            tl.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    };
     {
         bk::HostPool *pool = get_pool(c);
         PoolJob job(pool, (int)I, &fn);
         if (pool) pool->release((int)I);
+        mark();
         char *dx = (char *)c->X.p;
         for (int64_t g = 0; g < G; ++g) {
             const int64_t need = gstart[(size_t)g + 1] - gstart[(size_t)g];
@@ -1463,15 +1496,24 @@ int run_rows_small(bk_ctx *c, const char *const *rows, int dtype, int64_t n, int
             } else {
                 for (int64_t i = gstart[(size_t)g]; i < gstart[(size_t)g + 1]; ++i) fn((int)i);
             }
+            mark();
             const int64_t r0 = gstart[(size_t)g] * ri, r1 = std::min(n, gstart[(size_t)g + 1] * ri);
             CHK(timed(c, BK_K_H2D, [&] {
                 return hipMemcpyAsync(dx + (size_t)r0 * rowb, stage + (size_t)r0 * rowb,
                                       (size_t)(r1 - r0) * rowb, hipMemcpyHostToDevice, c->stream);
             }));
+            mark();
         }
     }
+    mark();
     const int st = run_host_small(c, c->X.p, BK_DEVICE, dld, dtype, nullptr, 0, 0, n, d, f, sel_idx,
                                   m_out, scores, mean_out, nullptr, 0);
+    mark();
+    if (trace) {
+        fprintf(stderr, "rows_trace G=%lld I=%lld:", (long long)G, (long long)I);
+        for (double t : tl) fprintf(stderr, " %.1f", t);
+        fprintf(stderr, "\n");
+    }
     drain.armed = st != BK_OK;
     return st;
 }

@@ -125,8 +125,10 @@ private:
     // bumped by every begin() / release(): what a spinning worker watches
     std::atomic<uint64_t> ticket_{0};
     std::atomic<bool> stop_flag_{false};
-    // ~20k pauses: ~0.1-0.7 ms depending on the core's pause latency
-    static constexpr int kSpin = 20000;
+    // ~4k pauses: tens of microseconds (a spinning worker burns the
+    // process's CPU share, which the caller and the copy engine's driver
+    // thread also need)
+    static constexpr int kSpin = 4000;
 };
 
 // Copy into pinned staging with non-temporal 16-B stores: the destination is

@@ -14,8 +14,10 @@
  *     (no krumReceived) it runs the same sort + computeScores on whatever
  *     arrived (n < threshold) and releases len(UpdateList) waiters.
  *   computeScores / getTopKRUMIndex  krum.go:77-166  through the shim's calls:
- *     bk_check_args -> bk_stage_alloc (C-owned pinned) -> pack rows ->
- *     bk_multikrum(BK_HOST_PINNED) -> bk_selection_margin; any error (e.g.
+ *     bk_check_args -> the UpdateList's row pointers -> bk_multikrum_rows
+ *     (libbk packs them on its host threads; BK_HARNESS_SERIAL_PACK=1 replays
+ *     the pre-r6 shim instead: bk_stage_alloc + a serial pack +
+ *     bk_multikrum(BK_HOST_PINNED)) -> bk_selection_margin; any error (e.g.
  *     n = 1: clip = int(0.5 * 1) = 0, the reference's argpartition ValueError)
  *     gives an empty AcceptedList: every update rejected.
  *   checkIfAccepted              krum.go:47-73
@@ -52,6 +54,7 @@ static const double *g_data;
 static int64_t g_d, g_thresh;
 static void *g_stage;
 static int64_t g_stage_len;
+static int g_serial_pack; /* BK_HARNESS_SERIAL_PACK=1: the shim's pre-r6 pinned pack */
 
 /* KRUMValidator state (krum.go:22-29) and the verifier globals it uses */
 static pthread_mutex_t krum_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -81,21 +84,35 @@ static void compute_scores(void)
     n_acc = 0;
     last_status = bk_check_args(n, d, f);
     if (last_status != BK_OK) return; /* reject all, as a failing Python call did */
-    const int64_t need = n * d * (int64_t)sizeof(double);
-    if (need > g_stage_len) {
-        if (g_stage) bk_stage_free(g_ctx, g_stage);
-        g_stage = NULL;
-        g_stage_len = 0;
-        last_status = bk_stage_alloc(g_ctx, need, &g_stage);
-        if (last_status != BK_OK) return;
-        g_stage_len = need;
-    }
-    double *stage = (double *)g_stage;
-    for (int64_t i = 0; i < n; ++i)
-        memcpy(stage + i * d, g_data + upd_row[i] * d, (size_t)d * sizeof(double));
     int64_t m = 0;
-    last_status = bk_multikrum(g_ctx, stage, BK_HOST_PINNED, BK_F64, n, d, d, f, accepted, &m,
-                               NULL, NULL);
+    if (g_serial_pack) {
+        /* the shim's pre-r6 form: pack the rows into a C-owned pinned batch */
+        const int64_t need = n * d * (int64_t)sizeof(double);
+        if (need > g_stage_len) {
+            if (g_stage) bk_stage_free(g_ctx, g_stage);
+            g_stage = NULL;
+            g_stage_len = 0;
+            last_status = bk_stage_alloc(g_ctx, need, &g_stage);
+            if (last_status != BK_OK) return;
+            g_stage_len = need;
+        }
+        double *stage = (double *)g_stage;
+        for (int64_t i = 0; i < n; ++i)
+            memcpy(stage + i * d, g_data + upd_row[i] * d, (size_t)d * sizeof(double));
+        last_status = bk_multikrum(g_ctx, stage, BK_HOST_PINNED, BK_F64, n, d, d, f, accepted, &m,
+                                   NULL, NULL);
+    } else {
+        /* the shim's form: the UpdateList's rows as they are (one pointer per
+         * update, in SourceID order), packed by libbk (bk_multikrum_rows) */
+        const void **rows = (const void **)malloc((size_t)n * sizeof(void *));
+        if (!rows) {
+            last_status = BK_ENOMEM;
+            return;
+        }
+        for (int64_t i = 0; i < n; ++i) rows[i] = g_data + upd_row[i] * d;
+        last_status = bk_multikrum_rows(g_ctx, rows, BK_F64, n, d, f, accepted, &m, NULL, NULL);
+        free(rows);
+    }
     if (last_status != BK_OK) return;
     double gap, bound;
     if (bk_selection_margin(g_ctx, &gap, &bound, &last_near) != BK_OK) last_near = -1;
@@ -214,6 +231,10 @@ int main(int argc, char **argv)
     }
     fclose(fp);
     g_data = data;
+    {
+        const char *e = getenv("BK_HARNESS_SERIAL_PACK");
+        g_serial_pack = e && atoi(e) != 0;
+    }
     if (bk_create(&g_ctx, 0) != BK_OK) { /* KRUMValidator.initialize (krum.go:31-44) */
         fprintf(stderr, "bk_create: %s\n", bk_last_error());
         return 1;

@@ -121,7 +121,7 @@ int bk_multikrum_rows(bk_ctx *ctx, const void *const *rows, int dtype, int64_t n
                       int64_t f, int64_t *sel_idx, int64_t *m_out, double *scores,
                       double *mean_out);
 /* Host threads that pack bk_multikrum_rows' rows, the caller's included (1:
- * the caller alone; 0: the default, BK_HOST_THREADS or min(16, hardware
+ * the caller alone; 0: the default, BK_HOST_THREADS or min(8, hardware
  * threads)).  The workers are started on the next call and sleep between
  * calls. */
 int bk_set_host_threads(bk_ctx *ctx, int threads);

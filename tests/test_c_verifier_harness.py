@@ -50,7 +50,8 @@ def test_harness_usage(harness):
 
 
 @pytest.mark.gpu
-def test_verifier_flow_against_oracle(harness, oracle, tmp_path):
+@pytest.mark.parametrize("serial_pack", ["0", "1"])  # bk_multikrum_rows / the pre-r6 pinned pack
+def test_verifier_flow_against_oracle(harness, oracle, tmp_path, serial_pack):
     rows, d, thresh = 12, 1000, 8
     X = oracle.synth(rows, d, 4242, 3)
     path = tmp_path / "updates.bin"
@@ -61,7 +62,8 @@ def test_verifier_flow_against_oracle(harness, oracle, tmp_path):
     # iteration 4: exactly 8 peers -> threshold path, nobody stale
     arrivals = [10, 5, 1, 8]
     r = subprocess.run([harness, str(path), str(rows), str(d), str(thresh), "400"]
-                       + [str(a) for a in arrivals], capture_output=True, text=True, timeout=120)
+                       + [str(a) for a in arrivals], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, BK_HARNESS_SERIAL_PACK=serial_pack))
     assert r.returncode == 0, r.stderr
     iters, peers = parse(r.stdout)
     assert sorted(iters) == [1, 2, 3, 4]
