@@ -1092,11 +1092,49 @@ def _free_port():
     return p
 
 
-def visible_gpus():
-    """GPUs this process could use, counted without initialising any of them
-    (torch.cuda.device_count() does not start the HIP runtime on this image)."""
-    import torch
-    return torch.cuda.device_count()
+def visible_gpus(environ=None, topology="/sys/class/kfd/kfd/topology/nodes", dri="/dev/dri"):
+    """GPUs this process could use, counted with no GPU runtime at all (VERDICT
+    r5 item 5): the launcher parent imports neither torch nor HIP and never
+    opens /dev/kfd.  A visibility list in the environment decides
+    (ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES, then CUDA_VISIBLE_DEVICES,
+    as the ROCm runtime applies them: the count of its comma-separated
+    entries, an empty list meaning none); otherwise the KFD topology's nodes
+    whose gpu_id is non-zero (CPU nodes have gpu_id 0) and whose render node
+    (/dev/dri/renderD<drm_render_minor>) this process may open -- the filter
+    the ROCm runtime applies in a container that exposes only some GPUs
+    (os.access: the node is not opened)."""
+    env = os.environ if environ is None else environ
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if var in env:
+            v = env[var].strip()
+            return len([x for x in v.split(",") if x.strip()]) if v else 0
+    count = 0
+    try:
+        nodes = os.listdir(topology)
+    except OSError:
+        return 0
+    for nd in nodes:
+        try:
+            with open(os.path.join(topology, nd, "gpu_id")) as fp:
+                if int(fp.read().strip() or "0") == 0:
+                    continue
+        except (OSError, ValueError):
+            continue
+        minor = None
+        try:
+            with open(os.path.join(topology, nd, "properties")) as fp:
+                for ln in fp:
+                    t = ln.split()
+                    if len(t) == 2 and t[0] == "drm_render_minor":
+                        minor = int(t[1])
+        except (OSError, ValueError):
+            pass
+        if minor is not None and minor > 0:
+            node = os.path.join(dri, "renderD%d" % minor)
+            if not os.access(node, os.R_OK | os.W_OK):
+                continue
+        count += 1
+    return count
 
 
 def launch_ranks(a, argv=None, gpus_fn=visible_gpus):
@@ -1308,7 +1346,11 @@ def main():
     # much as it computes: there two events on libbk's stream bracket the
     # whole timed loop instead (per-launch device time, gaps included, never
     # more than the step)
-    small_step = n <= 128 and not sharded
+    # (libbk's own predicate for the one-launch path, small_ok: n <= 128, d <=
+    # min(32768, BK_SMALL_MAX_D), BK_SMALL not 0 -- any mode: it is always
+    # exact; the evented breakdown below confirms which path ran -- ADVICE r5)
+    small_step = (not sharded and n <= 128 and os.environ.get("BK_SMALL", "1") != "0" and
+                  dl <= min(32768, int(os.environ.get("BK_SMALL_MAX_D") or 32768)))
     eng.timing_select(([] if small_step else ["k_gram"]) +
                       (["allreduce"] if sharded and not host_exch else []))
     tstride = 1
@@ -1335,6 +1377,13 @@ def main():
     torch.cuda.synchronize()
     kbreak = eng.timing_read()
     eng.timing_enable(False)
+    if small_step and "k_small" not in kbreak and "k_gram" in kbreak:
+        # the general chain ran after all: its K1 is the roofline kernel (the
+        # untimed pass's events), not the loop-bracketed clock
+        log("bench.py: n <= 128 but the one-launch path did not run; K1 from the evented pass")
+        kt.pop("k_small", None)
+        kt["k_gram"] = kbreak["k_gram"]
+        small_step = False
     # the selection margin of this batch (bk_selection_margin): near_tie False
     # proves the reference's argpartition selects exactly this set
     mg = eng.selection_margin()
@@ -1406,7 +1455,19 @@ def main():
                 log("bench.py: sharded variant %s failed: %r" % (tag, e))
                 variants[tag] = {"error": repr(e)}
                 break  # the ranks may no longer be in step: no further collective variants
-    if world > 1 and not a.no_variants and WORKLOADS[a.workload]["n"] > 128:
+    ranks_in_step = True
+    if world > 1 and not a.no_variants:
+        # every rank learns whether any rank's sharded variant failed before
+        # the collectives that follow (replica_variant's barrier and gathers):
+        # ranks that disagree about running them would hang
+        failed = any("error" in v for v in variants.values() if isinstance(v, dict))
+        flag = torch.tensor([1.0 if failed else 0.0], dtype=torch.float64,
+                            device=dev if not host_exch else "cpu")
+        tdist.all_reduce(flag, op=tdist.ReduceOp.MAX)
+        ranks_in_step = float(flag.item()) == 0.0
+        if not ranks_in_step:
+            log("bench.py: a rank's sharded variant failed; skipping the replica variant")
+    if world > 1 and not a.no_variants and WORKLOADS[a.workload]["n"] > 128 and ranks_in_step:
         # the reference's own scale-out: N independent verifiers, one batch each
         # (no exchange, so it runs under --exchange host too)
         variants[a.workload + "_replicas"] = replica_variant(eng, dev, a.workload, world, barrier)

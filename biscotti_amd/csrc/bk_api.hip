@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdarg>
@@ -163,6 +164,9 @@ struct bk_ctx {
     };
     std::vector<I8Cached> i8;
     DevBuf i8ws;
+    // K1i8 signatures {n, d, element size, digits} whose workspace failed to
+    // allocate: they run exact until the mode is set again (bk_set_f*_mode)
+    std::vector<std::array<int64_t, 4>> i8_failed;
     int gram_variant = 3;  // 3: LDS-shared v3 for aligned fp64; 1: v1 everywhere (BK_GRAM=v1)
     int gram_mode = 0;     // BK_GRAM_MODE: timing-only ablations of v3 (tools/, never tests)
     int f32_mode = BK_F32_EXACT;  // fp32 rows: widened onto the fp64 MFMA, or the fp32 MFMA
@@ -459,6 +463,12 @@ bk_ctx::I8Cached *i8_prepared(bk_ctx *c, const void *dX, int dtype, int64_t n, i
                               int64_t ld) {
     const int ns = i8_now(c, dX, dtype, d, ld);
     if (!ns) return nullptr;
+    // a layout whose workspace could not be allocated goes straight to the
+    // exact path on later calls: no repeated multi-GB hipMalloc attempts, no
+    // workspace freed (and captured graphs retired) every call
+    const std::array<int64_t, 4> sig{n, d, (int64_t)esize(dtype), ns};
+    for (const auto &f : c->i8_failed)
+        if (f == sig) return nullptr;
     const std::string keep = g_err;
     bk_ctx::I8Cached *e = nullptr;
     int st = c->test_i8_enomem ? BK_ENOMEM : get_i8(c, n, d, (int)esize(dtype), ns, &e);
@@ -466,6 +476,7 @@ bk_ctx::I8Cached *i8_prepared(bk_ctx *c, const void *dX, int dtype, int64_t n, i
     if (st == BK_OK) return e;
     (void)hipGetLastError();  // a failed hipMalloc must not surface at the next launch check
     g_err = keep;
+    c->i8_failed.push_back(sig);
     return nullptr;
 }
 
@@ -717,6 +728,11 @@ int stage_finish(bk_ctx *c, const double *U, const Plan &pl, const void *dX, int
         };
         if (sp.mode == SPLIT_RCCL) {
             // every rank joins the all-gather, whatever happened to its share
+            // (test knob BK_TEST_SPLIT_FAIL=p: this rank's share fails when p - 1
+            // is its rank -- tests/test_gpu_rccl_ranks.py, >= 2 GPUs)
+            if (st == BK_OK && c->test_split_fail == sp.part + 1)
+                st = fail(BK_EHIP, "test knob BK_TEST_SPLIT_FAIL=%d: this rank's share fails",
+                          c->test_split_fail);
             const std::string pre = st == BK_OK ? std::string() : g_err;
             const int s2 = share(sp.part, st == BK_OK);
             if (st == BK_OK) st = s2;
@@ -1863,6 +1879,7 @@ int bk_set_f32_mode(bk_ctx *c, int mode) {
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f32_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
     c->f32_mode = mode;
+    c->i8_failed.clear();  // a new mode tries K1i8's workspace again
     c->emu_split_n = -1;  // BK_EMU_SPLIT_SCORES: the new mode's first call scores every share
     return BK_OK;
 }
@@ -1875,6 +1892,7 @@ int bk_set_f64_mode(bk_ctx *c, int mode) {
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->f64_mode != mode) ++c->ws_epoch;  // captured graphs baked the other kernel in
     c->f64_mode = mode;
+    c->i8_failed.clear();
     c->emu_split_n = -1;
     return BK_OK;
 }

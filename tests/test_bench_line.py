@@ -86,3 +86,92 @@ def test_launcher_relays_the_ranks_failure(capfd):
                                      "--no-cpu-baseline"], gpus_fn=lambda: 1)
     out = capfd.readouterr().out
     assert rc != 0 and not out.strip()
+
+
+def test_visible_gpus_needs_no_gpu_runtime(tmp_path):
+    """the launcher counts GPUs from the environment or the
+    KFD topology (sysfs), never through torch / HIP: a fresh interpreter that
+    runs it has imported no torch and opened no /dev/kfd."""
+    import subprocess
+    topo = tmp_path / "nodes"
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    # 2 CPU nodes, 4 GPU nodes (one without a render minor), one CPU node; the
+    # GPU of minor 131 has no render node here (not exposed to this process)
+    for i, (gid, minor) in enumerate([(0, 0), (0, 0), (12345, 128), (0, 0), (777, 129),
+                                      (999, None), (555, 131)]):
+        (topo / str(i)).mkdir(parents=True)
+        (topo / str(i) / "gpu_id").write_text("%d\n" % gid)
+        if minor is not None:
+            (topo / str(i) / "properties").write_text("cpu_cores_count 0\ndrm_render_minor %d\n"
+                                                      % minor)
+        if minor in (128, 129):
+            (dri / ("renderD%d" % minor)).write_text("")
+    code = r"""
+import builtins, os, sys
+sys.path.insert(0, %r)
+opened = []
+real_open, real_os_open = builtins.open, os.open
+def spy(path, *a, **k):
+    opened.append(str(path))
+    return real_open(path, *a, **k)
+def spy_os(path, *a, **k):
+    opened.append(str(path))
+    return real_os_open(path, *a, **k)
+builtins.open, os.open = spy, spy_os
+import bench
+env = {k: v for k, v in os.environ.items() if not k.endswith("VISIBLE_DEVICES")}
+n_topo = bench.visible_gpus(environ=env, topology=%r, dri=%r)
+n_env = bench.visible_gpus(environ=dict(env, HIP_VISIBLE_DEVICES="0,3"))
+n_rocr = bench.visible_gpus(environ=dict(env, ROCR_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="1"))
+n_none = bench.visible_gpus(environ=env, topology=%r)
+print(n_topo, n_env, n_rocr, n_none, "torch" in sys.modules,
+      any("kfd" in p and p.startswith("/dev") for p in opened))
+""" % (REPO, str(topo), str(dri), str(tmp_path / "missing"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["3", "2", "0", "0", "False", "False"], r.stdout
+
+
+def test_launcher_parent_touches_no_gpu_runtime(tmp_path):
+    """`bench.py --gpus 2` as the launcher parent, its child replaced by a
+    stand-in: the parent counts GPUs, starts one child and relays its line,
+    and has imported no torch (so no torch.cuda) and opened no /dev/kfd."""
+    import subprocess
+    code = r"""
+import builtins, json, os, subprocess, sys
+sys.path.insert(0, %r)
+opened = []
+real_open = builtins.open
+def spy(path, *a, **k):
+    opened.append(str(path))
+    return real_open(path, *a, **k)
+builtins.open = spy
+started = []
+class FakeChild:
+    def __init__(self, cmd, **kw):
+        started.append(cmd)
+        self.stdout = iter(['{"n_gpus": 2}' + chr(10)])
+    def wait(self):
+        return 0
+    def send_signal(self, s):
+        pass
+subprocess.Popen = FakeChild
+import bench
+os.environ["HIP_VISIBLE_DEVICES"] = "0,1"
+sys.argv = ["bench.py", "--gpus", "2"]
+try:
+    bench.main()
+except SystemExit as e:
+    rc = e.code
+sys.stderr.write(json.dumps({"rc": rc, "children": len(started),
+                             "torch": "torch" in sys.modules,
+                             "kfd": any(p.startswith("/dev/kfd") for p in opened),
+                             "runs_torchrun": "torch.distributed.run" in " ".join(started[0])}))
+""" % REPO
+    env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=env)
+    res = json.loads(r.stderr.strip().splitlines()[-1])
+    assert res == {"rc": 0, "children": 1, "torch": False, "kfd": False, "runs_torchrun": True}, r
+    assert json.loads(r.stdout.strip()) == {"n_gpus": 2}

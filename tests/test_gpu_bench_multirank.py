@@ -84,6 +84,16 @@ def test_bench_launches_its_own_ranks():
     assert rep["sel"] == "match" and rep["value"] > 0, rep
 
 
+def test_launcher_gpu_count_matches_the_runtime():
+    """bench.py's launcher counts GPUs from the KFD topology / visibility
+    variables without any GPU runtime; on the GPU box it
+    must see exactly the devices the HIP runtime does."""
+    sys.path.insert(0, REPO)
+    import bench
+    import torch
+    assert bench.visible_gpus() == torch.cuda.device_count()
+
+
 def test_bench_refuses_more_rccl_ranks_than_gpus():
     """With the RCCL exchange every rank needs its own GPU: `--gpus N` with
     fewer visible GPUs exits non-zero instead of measuring one GPU."""
