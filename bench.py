@@ -312,7 +312,7 @@ E_SHARD_MODES = ("exact", "mfma", "i8x2_certified")
 
 
 def sharded_variant(eng, dev, name, f32_mode, nparts, rank, world, barrier, emu, steps=10,
-                    warmup=5):
+                    warmup=5, exchange_mode=0, line_mode=0):
     """A BASELINE config in its d-sharded multi-GPU form: this
     rank's column shard through libbk's sharded entry (K1 on the shard, the
     RCCL all-reduce of the packed Gram, split scoring at n >= 2049, the local
@@ -343,6 +343,9 @@ def sharded_variant(eng, dev, name, f32_mode, nparts, rank, world, barrier, emu,
 
     set_mode = eng.set_f64_mode if w["dtype"] == "f64" else eng.set_f32_mode
     set_mode(F32_MODES[f32_mode])
+    # exchange_mode 2: the all-reduce overlapped with the Gram in pieces
+    # (bk_comm_set_mode 2); line_mode: the line's own mode, restored after
+    eng.comm_set_mode(exchange_mode)
     try:
         r0 = eng.certified_reruns()
         for _ in range(max(5, warmup)):
@@ -350,7 +353,7 @@ def sharded_variant(eng, dev, name, f32_mode, nparts, rank, world, barrier, emu,
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        eng.timing_select(["k_gram", "allreduce", "score_gather"])
+        eng.timing_select(["k_gram", "allreduce", "score_gather", "exchange_exposed"])
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
@@ -370,6 +373,7 @@ def sharded_variant(eng, dev, name, f32_mode, nparts, rank, world, barrier, emu,
         reruns = eng.certified_reruns() - r0
     finally:
         set_mode(0)
+        eng.comm_set_mode(line_mode)
     if world > 1:
         el = max_over_ranks(el, dev)
     ms = el / steps * 1e3
@@ -382,6 +386,13 @@ def sharded_variant(eng, dev, name, f32_mode, nparts, rank, world, barrier, emu,
         return round(v["avg_ms"], 4) if v else None
     mine = {"rank": rank, "k_gram_ms": round(k1, 4), "exchange_ms": avg("allreduce"),
             "score_gather_ms": avg("score_gather")}
+    if exchange_mode == 2:
+        # the all-reduce span (first start -> last end, overlapping the Gram's
+        # later pieces) and the part of it left after the last piece
+        ex, sp_ = avg("exchange_exposed"), avg("allreduce")
+        mine["exchange_exposed_ms"] = ex
+        mine["overlapped_fraction"] = (round(1.0 - ex / sp_, 4) if ex is not None and sp_
+                                       else None)
     per_rank = [mine]
     if world > 1:
         hs, per_rank = [None] * world, [None] * world
@@ -995,6 +1006,10 @@ def _summ(v, host=None):
     if "per_rank" in v:  # a d-sharded variant: the slowest rank's exchange and score gather
         s["exchange_ms"] = v.get("exchange_ms")
         s["score_gather_ms"] = v.get("score_gather_ms")
+        ov = [p.get("overlapped_fraction") for p in v["per_rank"] if p]
+        if any(x is not None for x in ov):
+            s["exposed_ms"] = max((p.get("exchange_exposed_ms") or 0.0) for p in v["per_rank"] if p)
+            s["overlapped_fraction"] = min(x for x in ov if x is not None)
     if host:
         s["host_ms"] = host.get("ms_per_call")
         s["host_over_h2d_ms"] = host.get("overhead_over_h2d_ms")
@@ -1446,15 +1461,26 @@ def main():
     if sharded and not host_exch and not a.no_variants and a.workload == DEFAULT_WORKLOAD:
         # config E at this rank count (BASELINE: fp32, 8 x MI355X), each rank
         # its own column shard, beside the headline D (d-sharded the same way)
+        # each mode twice: the exchange after the whole Gram (mode 0), and
+        # overlapped with it in pieces (bk_comm_set_mode 2, tag "_overlap":
+        # per rank the all-reduce span, its exposed part and the overlapped
+        # fraction) -- the driver's N-GPU run decides between them
+        line_mode = 1 if a.deterministic else 0
+        stop = False
         for mode in E_SHARD_MODES:
-            tag = workload_tag("E_4096x262144_fp32", mode)
-            try:
-                variants[tag] = sharded_variant(eng, dev, "E_4096x262144_fp32", mode, emu or world,
-                                                rank, world, barrier, emu)
-            except Exception as e:  # noqa: BLE001 -- a variant's failure must not cost the headline line
-                log("bench.py: sharded variant %s failed: %r" % (tag, e))
-                variants[tag] = {"error": repr(e)}
-                break  # the ranks may no longer be in step: no further collective variants
+            for xm, suffix in ((0, ""), (2, "_overlap")):
+                tag = workload_tag("E_4096x262144_fp32", mode) + suffix
+                try:
+                    variants[tag] = sharded_variant(eng, dev, "E_4096x262144_fp32", mode,
+                                                    emu or world, rank, world, barrier, emu,
+                                                    exchange_mode=xm, line_mode=line_mode)
+                except Exception as e:  # noqa: BLE001 -- a variant's failure must not cost the headline line
+                    log("bench.py: sharded variant %s failed: %r" % (tag, e))
+                    variants[tag] = {"error": repr(e)}
+                    stop = True  # the ranks may no longer be in step: no further collective variants
+                    break
+            if stop:
+                break
     ranks_in_step = True
     if world > 1 and not a.no_variants:
         # every rank learns whether any rank's sharded variant failed before

@@ -16,13 +16,13 @@ BK_MAX_N = 16384
 BK_UNIQUE_ID_BYTES = 128
 BK_SYNTH_FP32ROUND = 1
 BK_GROUP_ALLREDUCE, BK_GROUP_DETERMINISTIC, BK_GROUP_HOST_EXCHANGE = 0, 1, 2
-BK_ABI_VERSION = 13
+BK_ABI_VERSION = 14
 BK_F32_EXACT, BK_F32_MFMA, BK_F32_CERTIFIED, BK_F32_I8, BK_F32_I8_CERTIFIED = 0, 1, 2, 3, 4
 BK_F32_I8X2, BK_F32_I8X2_CERTIFIED = 5, 6  # two digit planes, three products (bk.h)
 BK_F64_EXACT, BK_F64_I8, BK_F64_I8_CERTIFIED, BK_F64_I8X2, BK_F64_I8X2_CERTIFIED = 0, 3, 4, 5, 6
 KERNELS = ["k_gram", "k_reduce", "k_transpose", "k_scores", "k_rank", "k_compact", "k_mean",
            "allreduce", "k_synth", "h2d", "d2h", "k_aggregate", "k_qsum", "k_noise", "k_roni",
-           "k_small", "k_slice", "score_gather"]
+           "k_small", "k_slice", "score_gather", "exchange_exposed"]
 K = {name: i for i, name in enumerate(KERNELS)}
 
 # every symbol include/bk.h declares: name -> (restype, argtypes)

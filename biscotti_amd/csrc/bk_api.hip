@@ -1,6 +1,7 @@
 // bk_api.hip -- the C ABI (include/bk.h): context, workspace, orchestration,
 // RCCL exchange, per-kernel HIP-event timing.  No torch, no C++ types across
 // the boundary; every failure becomes a negative status + bk_last_error().
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -64,13 +65,32 @@ const char *kKernelNames[BK_NUM_KERNELS] = {"k_gram",    "k_reduce",  "k_transpo
                                             "k_rank",    "k_compact", "k_mean",   "allreduce",
                                             "k_synth",   "h2d",       "d2h",
                                             "k_aggregate", "k_qsum",  "k_noise",
-                                            "k_roni", "k_small", "k_slice", "score_gather"};
+                                            "k_roni", "k_small", "k_slice", "score_gather",
+                                            "exchange_exposed"};
 
 struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
     uint64_t *epoch = nullptr;  // the owning context's ws_epoch (graph invalidation)
 };
+
+// A K1 plan's (or K1i8 layout's) split into k launches whose sub-tiles are
+// contiguous pieces of the packed upper, for the exchange overlapped with
+// the Gram (bk_comm_set_mode 2): piece p's elements are U[e[p], e[p + 1]),
+// the last piece's range ending with the trailing record
+struct Pieces {
+    int k = 0;                // pieces built for (0: none yet)
+    bool ok = false;          // false: the plan has no k-piece split
+    std::vector<int64_t> e;   // k + 1 element bounds of U
+    std::vector<int> nwg;     // per piece: launched workgroups (K1 v3) / items (K1i8)
+    std::vector<size_t> off;  // per piece: its table's offset in d (ints)
+    int *d = nullptr;         // device copy of the tables, concatenated
+};
+
+void free_pieces(Pieces &pc) {
+    if (pc.d) (void)hipFree(pc.d);
+    pc = Pieces();
+}
 
 }  // namespace
 
@@ -154,6 +174,7 @@ struct bk_ctx {
         int64_t d;
         int bk;  // columns per k-block (16 fp64, 32 fp32)
         Plan3 p;
+        Pieces pc;
     };
     std::vector<CachedPlan> plans;
     // K1i8 (BK_F32_I8): layouts and device tables per (n, d), and the workspace
@@ -161,6 +182,7 @@ struct bk_ctx {
         int64_t n = 0, d = 0;
         I8Layout L;
         void *tables = nullptr;
+        Pieces pc;
     };
     std::vector<I8Cached> i8;
     DevBuf i8ws;
@@ -198,6 +220,7 @@ struct bk_ctx {
     DevBuf status;
     int test_fail_exchange = 0;  // test knob BK_TEST_FAIL_BEFORE_EXCHANGE (bk_create)
     int test_i8_enomem = 0;      // test knob BK_TEST_I8_ENOMEM: K1i8's workspace "fails" (bk_create)
+    int test_fail_piece = 0;     // test knob BK_TEST_FAIL_PIECE=p: the overlapped Gram's piece p-1 fails
     // split scoring (stage_finish): at n >= split_min_n each rank of a sharded
     // call scores its share of the rows and the ranks all-gather the scores
     // (BK_SPLIT_SCORES_MIN_N; 0 turns it off).  Knobs for a 1-rank
@@ -213,6 +236,14 @@ struct bk_ctx {
     int test_split_fail = 0;   // BK_TEST_SPLIT_FAIL=p: under BK_TEST_SPLIT_SCORES, share p - 1 "fails"
     int64_t emu_split_n = -1;  // emulation: the n whose other chunks are scored
     DevBuf sgather;            // the gathered scores: parts x chunk doubles
+    // bk_comm_set_mode 2: the exchange overlapped with the Gram in this many
+    // pieces (BK_OVERLAP_PIECES, default 2; 0: off), all-reduced on cstream
+    int overlap = 0;
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_piece[8] = {};
+    hipEvent_t ev_cdone = nullptr;
+    unsigned *sigcnt[8] = {};       // the pieces' completion counts (signal memory, 8 B each)
+    int wait_value_ok = -1;         // hipDeviceAttributeCanUseStreamWaitValue (-1: not asked)
     int64_t exchanges = 0;        // exchanges of the packed Gram (bk_comm_stats)
     double exchanged_bytes = 0;   // bytes each rank put into them
 };
@@ -387,6 +418,7 @@ int get_plan3(bk_ctx *c, int64_t n, int64_t d, int bk, Plan3 **out) {
     }
     if (c->plans.size() >= 8) {
         free_plan(c->plans.front().p);
+        free_pieces(c->plans.front().pc);
         c->plans.erase(c->plans.begin());
         ++c->ws_epoch;  // a captured graph may point at the evicted tables
     }
@@ -446,6 +478,7 @@ int get_i8(bk_ctx *c, int64_t n, int64_t d, int es, int ns, bk_ctx::I8Cached **o
     }
     if (c->i8.size() >= 4) {
         (void)hipFree(c->i8.front().tables);
+        free_pieces(c->i8.front().pc);
         c->i8.erase(c->i8.begin());
         ++c->ws_epoch;  // a captured graph may point at the evicted tables
     }
@@ -566,6 +599,86 @@ int stage_gram(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64
     CHK(timed(c, BK_K_GRAM,
               [&] { return launch_gram(dX, dtype, ld, (int)n, d, pl, part, c->stream); }));
     CHK(timed(c, BK_K_REDUCE, [&] { return launch_reduce(part, pl, U, c->stream); }));
+    return BK_OK;
+}
+
+// ---- the Gram in pieces, for an exchange overlapped with it ---------------
+// (bk_comm_set_mode 2).  The packed upper is
+// cut into k contiguous pieces by rows of sub-tiles; piece p is computed by its
+// own launches (the same segments / (tile, range) items as the one launch, so
+// every sub-tile is bitwise the same), and its all-reduce starts on the
+// communication stream while the next pieces compute.
+
+// the device copy of the pieces' tables
+int upload_pieces(Pieces &pc, const std::vector<std::vector<int>> &tabs, int per_item) {
+    size_t tot = 0;
+    for (auto &t : tabs) {
+        pc.off.push_back(tot);
+        pc.nwg.push_back((int)(t.size() / per_item));
+        tot += t.size();
+    }
+    std::vector<int> all;
+    all.reserve(tot);
+    for (auto &t : tabs) all.insert(all.end(), t.begin(), t.end());
+    hipError_t e = hipMalloc(&pc.d, std::max<size_t>(tot, 1) * sizeof(int));
+    if (e == hipSuccess && tot)
+        e = hipMemcpy(pc.d, all.data(), tot * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        free_pieces(pc);
+        return fail(BK_ENOMEM, "piece tables: %s", hipGetErrorString(e));
+    }
+    pc.ok = true;
+    return BK_OK;
+}
+
+// The k-piece split of this call's Gram (built once per plan / layout and k):
+// *out = nullptr when the call's Gram has none (K1 v1, a McNaughton plan
+// whose workgroups span pieces, too few row blocks); then the caller computes
+// the Gram whole and exchanges it after
+int gram_pieces(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t d, int64_t ld, int k,
+                const Pieces **out) {
+    *out = nullptr;
+    const int64_t usz = bk_upper_elems(n);
+    auto finish = [&](Pieces &pc, const std::vector<int> &tile_end) {
+        pc.e.assign(1, 0);
+        for (size_t p = 0; p < tile_end.size(); ++p)
+            pc.e.push_back(p + 1 < tile_end.size() ? (int64_t)tile_end[p] * 4096 : usz);
+    };
+    if (bk_ctx::I8Cached *e = i8_prepared(c, dX, dtype, n, d, ld)) {
+        Pieces &pc = e->pc;
+        if (pc.k != k) {
+            free_pieces(pc);
+            pc.k = k;
+            std::vector<int> tile_end;
+            std::vector<std::vector<int>> orders;
+            if (i8_pieces(e->L, k, tile_end, orders)) {
+                CHK(upload_pieces(pc, orders, 2));
+                finish(pc, tile_end);
+            }
+        }
+        if (pc.ok) *out = &pc;
+        return BK_OK;
+    }
+    if (!use_v3(c, dX, dtype, ld)) return BK_OK;
+    Plan3 *p3 = nullptr;
+    const int bk = v3_bk(dtype);
+    CHK(get_plan3(c, n, d, bk, &p3));
+    for (auto &cp : c->plans)
+        if (&cp.p == p3) {
+            Pieces &pc = cp.pc;
+            if (pc.k != k) {
+                free_pieces(pc);
+                pc.k = k;
+                const Plan3Host H = build_plan3((int)n, d, c->num_cu, bk);
+                std::vector<int> tile_end;
+                std::vector<std::vector<int>> segs;
+                if (plan3_pieces(H, k, tile_end, segs)) {
+                    CHK(upload_pieces(pc, segs, 2));
+                    finish(pc, tile_end);
+                }
+            }
+            if (pc.ok) *out = &pc;
+        }
     return BK_OK;
 }
 
@@ -1666,6 +1779,7 @@ int bk_create(bk_ctx **out, int device) {
     if (const char *v = getenv("BK_SMALL_CHECK_LINES")) c->small_check_lines = atoi(v) != 0;
     if (const char *v = getenv("BK_TEST_FAIL_BEFORE_EXCHANGE")) c->test_fail_exchange = atoi(v);
     if (const char *v = getenv("BK_TEST_I8_ENOMEM")) c->test_i8_enomem = atoi(v) != 0;
+    if (const char *v = getenv("BK_TEST_FAIL_PIECE")) c->test_fail_piece = atoi(v);
     if (const char *v = getenv("BK_SPLIT_SCORES_MIN_N")) c->split_min_n = atoll(v);
     if (const char *v = getenv("BK_TEST_SPLIT_SCORES")) c->test_split_scores = atoi(v);
     if (const char *v = getenv("BK_EMU_SPLIT_SCORES")) c->emu_split_scores = atoi(v);
@@ -1702,6 +1816,13 @@ void bk_destroy(bk_ctx *c) {
         for (hipEvent_t ev : {c->ev_go, c->ev_cp[0], c->ev_cp[1], c->ev_use[0], c->ev_use[1],
                               c->ev_rows[0], c->ev_rows[1], c->ev_rows[2], c->ev_rows[3]})
             if (ev) (void)hipEventDestroy(ev);
+        if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+        for (hipEvent_t ev : c->ev_piece)
+            if (ev) (void)hipEventDestroy(ev);
+        if (c->ev_cdone) (void)hipEventDestroy(c->ev_cdone);
+        if (c->cstream) (void)hipStreamDestroy(c->cstream);
+        for (unsigned *sgc : c->sigcnt)
+            if (sgc) (void)hipFree(sgc);
         if (c->rstage) (void)hipHostFree(c->rstage);
         delete c->hpool;
         if (c->copy) (void)hipStreamDestroy(c->copy);
@@ -1711,9 +1832,14 @@ void bk_destroy(bk_ctx *c) {
             (void)hipEventDestroy(ev.b);
         }
         for (hipEvent_t ev : c->pool) (void)hipEventDestroy(ev);
-        for (auto &cp : c->plans) free_plan(cp.p);
-        for (auto &e : c->i8)
+        for (auto &cp : c->plans) {
+            free_plan(cp.p);
+            free_pieces(cp.pc);
+        }
+        for (auto &e : c->i8) {
             if (e.tables) (void)hipFree(e.tables);
+            free_pieces(e.pc);
+        }
         for (auto &cg : c->graphs) drop_graph(cg);
         if (c->comm) (void)ncclCommDestroy(c->comm);
         if (c->own) (void)hipStreamDestroy(c->own);
@@ -2087,13 +2213,193 @@ int bk_comm_init(bk_ctx *c, int nranks, int rank, const void *id) {
     return BK_OK;
 }
 
-int bk_comm_set_mode(bk_ctx *c, int deterministic) {
+int bk_comm_set_mode(bk_ctx *c, int mode) {
     if (!c) return fail(BK_EINVAL, "null context");
-    c->deterministic = deterministic ? 1 : 0;
+    if (mode < 0 || mode > 2) return fail(BK_EINVAL, "bad exchange mode %d", mode);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->deterministic = mode == 1 ? 1 : 0;
+    int k = 2;
+    if (const char *v = getenv("BK_OVERLAP_PIECES")) k = atoi(v);
+    c->overlap = mode == 2 ? std::max(2, std::min(8, k)) : 0;
     return BK_OK;
 }
 
 namespace {
+// the communication stream of the overlapped exchange and its events (once)
+int ensure_comm_stream(bk_ctx *c) {
+    if (c->cstream) return BK_OK;
+    // one signal-memory allocation per piece count (HIP hands signal memory
+    // out 8 bytes at a time)
+    for (int i = 0; i < 8; ++i)
+        if (!c->sigcnt[i]) {
+            void *sp = nullptr;
+            HIPCHK(hipExtMallocWithFlags(&sp, 8, hipMallocSignalMemory));
+            c->sigcnt[i] = (unsigned *)sp;
+        }
+    hipStream_t cs = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipError_t e = hipSuccess;
+    hipEvent_t ev[9] = {};
+    for (int i = 0; i < 9 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        for (hipEvent_t x : ev)
+            if (x) (void)hipEventDestroy(x);
+        (void)hipStreamDestroy(cs);
+        return fail(BK_EHIP, "communication stream events: %s", hipGetErrorString(e));
+    }
+    for (int i = 0; i < 8; ++i) c->ev_piece[i] = ev[i];
+    c->ev_cdone = ev[8];
+    c->cstream = cs;
+    return BK_OK;
+}
+
+// The sharded call with its exchange overlapped with the Gram (bk_comm_set_mode
+// 2).  ONE Gram launch runs the pieces' workgroups in piece order, each
+// workgroup counting itself into its piece's signal word at exit (PieceMarks).
+// The communication stream waits for piece p's count (hipStreamWaitValue32),
+// reduces piece p's sub-tiles (K1b, or K1i8's reduce of its range) and
+// all-reduces them while the Gram's later pieces still run; the last piece is
+// reduced on the context stream after the Gram, with the trailing record, and
+// all-reduced last.  Every sub-tile is summed from the same partials in the
+// same order as the serial path and the all-reduce sums element by element,
+// so every output is bitwise that of mode 0.  A failure before the Gram's
+// launch is queued poisons the record and joins every piece's all-reduce with
+// no wait; the waits are queued only behind a launched Gram, whose every
+// workgroup counts itself (idle ones included), so they always resolve.
+int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, int64_t n,
+                       int64_t dl, int64_t ld, int64_t f, double *U, Plan &pl, int64_t *d_sel,
+                       double *d_scores, double *d_mean, const ScoreSplit &sp) {
+    const int k = pc.k;
+    pl.n = (int)n;
+    pl.d = dl;
+    pl.T = (int)((n + 63) / 64);
+    pl.ntile = pl.T * (pl.T + 1) / 2;
+    PieceMarks pm;
+    for (int p = 0; p < k; ++p) pm.cnt[p] = c->sigcnt[p];
+    pm.k = k;
+    int tot = 0;
+    for (int p = 0; p < k; ++p) {
+        pm.start[p] = tot;
+        tot += pc.nwg[(size_t)p];
+    }
+    pm.start[k] = tot;
+    bk_ctx::I8Cached *e8 = i8_prepared(c, dX, dtype, n, dl, ld);
+    Plan3 *p3 = nullptr;
+    double *part = nullptr;
+    const bool f32m = f32_mfma_now(c, dtype);
+    int st = BK_OK;
+    if (!e8) {
+        st = get_plan3(c, n, dl, v3_bk(dtype), &p3);
+        if (st == BK_OK) st = ensure(c->part, (size_t)p3->nvwg * 16 * 4096 * sizeof(double));
+        if (st == BK_OK) part = (double *)c->part.p;
+    }
+    // 1. zero the piece counts; K1i8: the digit slices; then the one Gram launch
+    bool launched = false;
+    for (int p = 0; p < k && st == BK_OK; ++p) {
+        const hipError_t e = hipMemsetAsync(c->sigcnt[p], 0, 8, c->stream);
+        if (e != hipSuccess) st = fail(BK_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+    }
+    if (st == BK_OK && c->test_fail_piece)  // test knob BK_TEST_FAIL_PIECE (bk_create)
+        st = fail(BK_EHIP, "test knob BK_TEST_FAIL_PIECE=%d: the Gram fails before its launch",
+                  c->test_fail_piece);
+    if (st == BK_OK && e8)
+        st = timed(c, BK_K_SLICE, [&] {
+            return launch_i8_slice(dX, dtype, ld, (int)n, dl, e8->L, c->i8ws.p, e8->tables, c->stream);
+        });
+    // probe build: BK_PIECES_NOMARK=1 -- the pieces' workgroup order with no
+    // counts, every piece reduced on the context stream after the Gram (an A/B
+    // of the order alone; timing only)
+    const bool nomark = probe_env("BK_PIECES_NOMARK") != nullptr;
+    if (nomark) pm.k = 0;
+    if (st == BK_OK) {
+        st = timed(c, BK_K_GRAM, [&] {
+            return e8 ? launch_i8_gemm((int)n, e8->L, c->i8ws.p, e8->tables, c->stream, pc.d, tot, pm)
+                      : launch_gram3(dX, dtype, ld, (int)n, dl, *p3, part, c->stream, c->gram_mode,
+                                     nullptr, f32m, pc.d, tot, pm);
+        });
+        launched = st == BK_OK;
+    }
+    if (nomark && launched) {
+        for (int p = 0; p < k; ++p) {
+            const int64_t e0 = pc.e[(size_t)p], e1 = p + 1 == k ? (int64_t)pl.ntile * 4096 : pc.e[(size_t)p + 1];
+            HIPCHK(e8 ? launch_i8_reduce(dl, e8->L, c->i8ws.p, U, c->stream, e0, e1, p + 1 == k)
+                      : launch_reduce3(part, *p3, U, c->stream, f32m, (int)(e0 / 4096), (int)(e1 / 4096),
+                                       p + 1 == k));
+        }
+        const int64_t usz = bk_upper_elems(n);
+        RCCLCHK(ncclAllReduce(U, U, (size_t)usz, ncclDouble, ncclSum, c->comm, c->stream));
+        ++c->exchanges;
+        return stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, d_mean, sp);
+    }
+    const std::string st_msg = st == BK_OK ? std::string() : g_err;
+    if (st != BK_OK) CHK(poison_upper(c, U, n));
+    // the communication stream starts behind everything queued so far (the
+    // counts' reset above, or the poisoned record)
+    HIPCHK(hipEventRecord(c->ev_piece[0], c->stream));
+    HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_piece[0], 0));
+    hipEvent_t ar_a = nullptr, ar_b = nullptr, ex_a = nullptr, ex_b = nullptr;
+    const bool t_ar = timing_on(c, BK_K_ALLREDUCE), t_ex = timing_on(c, BK_K_EXCHANGE_EXPOSED);
+    auto reduce_piece = [&](int p, hipStream_t s, bool rec) -> hipError_t {
+        const int64_t e0 = pc.e[(size_t)p], e1 = rec ? (int64_t)pl.ntile * 4096 : pc.e[(size_t)p + 1];
+        if (e8) return launch_i8_reduce(dl, e8->L, c->i8ws.p, U, s, e0, e1, rec);
+        return launch_reduce3(part, *p3, U, s, f32m, (int)(e0 / 4096), (int)(e1 / 4096), rec);
+    };
+    // pieces 0 .. k-2 on the communication stream, each as soon as its
+    // workgroups are done; the last piece (and the record) on the context
+    // stream after the Gram, all-reduced there too once the communication
+    // stream's all-reduces are done -- one stream hop at the end, not two
+    for (int p = 0; p + 1 < k; ++p) {
+        if (launched) {
+            HIPCHK(hipStreamWaitValue32(c->cstream, c->sigcnt[p], (uint32_t)pc.nwg[(size_t)p],
+                                        hipStreamWaitValueGte, 0xffffffffu));
+            HIPCHK(reduce_piece(p, c->cstream, false));
+        }
+        if (p == 0 && t_ar) {
+            CHK(get_event(c, &ar_a));
+            HIPCHK(hipEventRecord(ar_a, c->cstream));
+        }
+        const int64_t e0 = pc.e[(size_t)p], e1 = pc.e[(size_t)p + 1];
+        RCCLCHK(ncclAllReduce(U + e0, U + e0, (size_t)(e1 - e0), ncclDouble, ncclSum, c->comm,
+                              c->cstream));
+    }
+    HIPCHK(hipEventRecord(c->ev_cdone, c->cstream));
+    if (launched) {
+        const hipError_t e = reduce_piece(k - 1, c->stream, true);
+        if (e != hipSuccess) {
+            CHK(poison_upper(c, U, n));
+            st = fail(BK_EHIP, "K1b of the last piece: %s", hipGetErrorString(e));
+        }
+    }
+    if (t_ex) {  // the exposed part: the last piece reduced -> its all-reduce done
+        CHK(get_event(c, &ex_a));
+        HIPCHK(hipEventRecord(ex_a, c->stream));
+    }
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_cdone, 0));
+    {
+        const int64_t e0 = pc.e[(size_t)k - 1], e1 = pc.e[(size_t)k];
+        RCCLCHK(ncclAllReduce(U + e0, U + e0, (size_t)(e1 - e0), ncclDouble, ncclSum, c->comm,
+                              c->stream));
+    }
+    if (t_ar) {  // the span: the first all-reduce's start -> the last one's end
+        CHK(get_event(c, &ar_b));
+        HIPCHK(hipEventRecord(ar_b, c->stream));
+        c->pending.push_back({BK_K_ALLREDUCE, ar_a, ar_b});
+    }
+    if (t_ex) {
+        CHK(get_event(c, &ex_b));
+        HIPCHK(hipEventRecord(ex_b, c->stream));
+        c->pending.push_back({BK_K_EXCHANGE_EXPOSED, ex_a, ex_b});
+    }
+    c->exchanged_bytes += (double)bk_upper_elems(n) * sizeof(double);
+    ++c->exchanges;
+    if (st != BK_OK) {
+        (void)stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, nullptr, sp);
+        g_err = st_msg.empty() ? g_err : st_msg;
+        return st;
+    }
+    return stage_finish(c, U, pl, dX, dtype, n, dl, ld, f, d_sel, d_scores, d_mean, sp);
+}
+
 // one pass of the sharded entry: partial Gram of the local columns (zeros for
 // an empty shard), the exchange, then scores/selection and the local mean.
 //
@@ -2114,13 +2420,29 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
     const bool exch = c->comm != nullptr;
     const bool agree = exch && (c->nranks > 1 || c->test_fail_exchange) &&
                        (n != c->agreed_n || f != c->agreed_f || dtype != c->agreed_dtype ||
-                        c->deterministic != c->agreed_det);
+                        c->deterministic + 2 * c->overlap != c->agreed_det);
     const ScoreSplit sp = score_split(c, n);
     int prep = ensure(c->U, (size_t)usz * sizeof(double));
     if (prep == BK_OK && exch && c->deterministic)
         prep = ensure(c->Ug, (size_t)usz * c->nranks * sizeof(double));
     if (prep == BK_OK && sp.parts > 1) prep = prepare_finish(c, n, sp, d_scores == nullptr);
     if (prep == BK_OK && dl > 0) prep = prepare_gram(c, dX, dtype, n, dl, ld);
+    // bk_comm_set_mode 2: the Gram in pieces, each all-reduced on the
+    // communication stream while the next computes (nullptr: this call's
+    // Gram has no such split -- it is computed whole and exchanged after)
+    const Pieces *pcs = nullptr;
+    if (prep == BK_OK && exch && c->overlap >= 2 && !c->deterministic && dl > 0) {
+        if (c->wait_value_ok < 0) {
+            int v = 0;
+            c->wait_value_ok = hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue,
+                                                     c->device) == hipSuccess && v ? 1 : 0;
+            (void)hipGetLastError();
+        }
+        if (c->wait_value_ok) {
+            prep = gram_pieces(c, dX, dtype, n, dl, ld, c->overlap, &pcs);
+            if (prep == BK_OK && pcs) prep = ensure_comm_stream(c);
+        }
+    }
     if (prep == BK_OK && c->test_fail_exchange == (agree ? 1 : 2))
         prep = fail(BK_ENOMEM, "test knob BK_TEST_FAIL_BEFORE_EXCHANGE=%d: forced failure",
                     c->test_fail_exchange);
@@ -2142,7 +2464,7 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
         c->agreed_n = n;
         c->agreed_f = f;
         c->agreed_dtype = dtype;
-        c->agreed_det = c->deterministic;
+        c->agreed_det = c->deterministic + 2 * c->overlap;
     } else if (prep != BK_OK && (!exch || c->U.bytes < (size_t)usz * sizeof(double))) {
         return prep;  // nothing to join (no communicator), or no partial to poison
     }
@@ -2152,6 +2474,9 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
     pl.T = (int)((n + 63) / 64);
     pl.ntile = pl.T * (pl.T + 1) / 2;
     int st = prep;
+    if (pcs && st == BK_OK)
+        return sharded_overlapped(c, *pcs, dX, dtype, n, dl, ld, f, U, pl, d_sel, d_scores, d_mean,
+                                  sp);
     if (st == BK_OK) {
         if (dl > 0) {
             st = stage_gram(c, dX, dtype, n, dl, ld, U, pl);

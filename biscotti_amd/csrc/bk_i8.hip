@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
 void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                const int64_t *__restrict__ rb, int R, const int2 *__restrict__ order,
                const int *__restrict__ es, int n, int T64, double *__restrict__ part,
-               int64_t ntile64) {
+               int64_t ntile64, PieceMarks pm) {
     constexpr int NT = 64 * NW;                        // threads
     constexpr int TJ = (NW / 2) * 32 * NBJ;            // the tile's columns (rows of operand B)
     constexpr int NGR = I8_STAGE / 16 / NT;            // 16-B granules each thread stages per chunk
@@ -339,7 +339,10 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
     // TJ: I | J << 16) and column range (i8_layout; r < 0: a padding workgroup
     // of a short XCD list)
     const int2 item = order[blockIdx.x];
-    if (item.y < 0) return;
+    if (item.y < 0) {
+        piece_done(pm);
+        return;
+    }
     const int r = item.y, I = item.x & 0xffff, J = item.x >> 16;
     const int64_t k0 = rb[r], k1 = rb[r + 1];
     const int nch = (int)((k1 - k0) / I8_KC);
@@ -535,14 +538,18 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                     (ei == I8_NONFINITE || ej == I8_NONFINITE) ? __builtin_nan("") : ldexp(v, ei + ej + sh);
             }
         }
+    piece_done(pm);
 }
 
 // U = sum over the R ranges, in order; the trailing record {d, 0, bound, 0}
+// (e0 / e1 / rec: one piece of the packed upper when the exchange overlaps
+// the Gram -- the same sums, the record only with the last piece)
 __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ part, int R,
                                                    int64_t usz, double *__restrict__ U, double d,
-                                                   const double *__restrict__ bound) {
-    const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
-    if (e < usz) {
+                                                   const double *__restrict__ bound, int64_t e0,
+                                                   int64_t e1, int rec) {
+    const int64_t e = e0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (e < e1) {
         // ranges in order, 8 loads in flight per thread (R is a multiple of 8)
         d2v acc = *reinterpret_cast<const d2v *>(part + e);
         for (int r0 = 1; r0 < R; r0 += 8) {
@@ -561,7 +568,7 @@ __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ pa
         }
         *reinterpret_cast<d2v *>(U + e) = acc;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (rec && blockIdx.x == 0 && threadIdx.x == 0) {
         U[usz] = d;
         U[usz + 1] = 0.0;
         U[usz + 2] = bound[0];
@@ -583,6 +590,48 @@ __global__ __launch_bounds__(256) void k_i8_reduce(const double *__restrict__ pa
 #ifndef BK_I8_RQ
 #define BK_I8_RQ 8  // column ranges come in multiples of this (A/B builds)
 #endif
+// The workgroup order of a tile list over R ranges.  Workgroup b runs on XCD
+// b mod 8 (dispatch order; speed only).  Every XCD sweeps the ranges in the
+// same order, taking a contiguous piece of the tile order per range (ceil or
+// floor of NT / 8 tiles, the extra tiles rotating over the XCDs so the totals
+// balance): at any time the whole chip works on one column range, so the
+// digit lines one XCD fetches are found in the Infinity Cache by the others,
+// while each XCD's concurrent tiles stay compact (few row-blocks per chunk in
+// its L2)
+static std::vector<int> i8_sweep_order(const std::vector<int> &tiles, int R) {
+    std::vector<int> order;
+    const int NT = (int)tiles.size();
+#if BK_I8_MAP == 0
+    // r3/r4a: workgroup b runs range b mod R (= its XCD when R = 8) and tile b / R
+    for (int b = 0; b < NT * R; ++b) {
+        order.push_back(tiles[b / R]);
+        order.push_back(b % R);
+    }
+#else
+    std::vector<std::vector<int>> per(8);
+    for (int r = 0; r < R; ++r) {
+        const int q = NT / 8, rem = NT % 8;
+        int j = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int cnt = q + (((x - r) % 8 + 8) % 8 < rem ? 1 : 0);
+            for (int k = 0; k < cnt; ++k, ++j) {
+                per[x].push_back(tiles[j]);
+                per[x].push_back(r);
+            }
+        }
+    }
+    size_t mx = 0;
+    for (auto &v : per) mx = std::max(mx, v.size() / 2);
+    for (size_t sidx = 0; sidx < mx; ++sidx)
+        for (int x = 0; x < 8; ++x) {
+            const bool on = sidx < per[x].size() / 2;
+            order.push_back(on ? per[x][2 * sidx] : 0);
+            order.push_back(on ? per[x][2 * sidx + 1] : -1);
+        }
+#endif
+    return order;
+}
+
 I8Layout i8_layout(int n, int64_t d, int es, int num_cu, int ns) {
     I8Layout L;
     L.ns = ns == 2 ? 2 : 3;
@@ -650,42 +699,36 @@ I8Layout i8_layout(int n, int64_t d, int es, int num_cu, int ns) {
     L.T128 = L.npad / I8_TILE;
     L.T64 = (n + 63) / 64;
     L.ntile64 = (int64_t)L.T64 * (L.T64 + 1) / 2;
-#if BK_I8_MAP == 0
-    // r3/r4a: workgroup b runs range b mod R (= its XCD when R = 8) and tile b / R
-    for (int b = 0; b < NT * L.R; ++b) {
-        L.order.push_back(tiles[b / L.R]);
-        L.order.push_back(b % L.R);
-    }
-#else
-    // Workgroup b runs on XCD b mod 8 (dispatch order; speed only).  Every XCD
-    // sweeps the ranges in the same order, taking a contiguous piece of the
-    // tile order per range (ceil or floor of NT / 8 tiles, the extra tiles
-    // rotating over the XCDs so the totals balance): at any time the whole
-    // chip works on one column range, so the digit lines one XCD fetches are
-    // found in the Infinity Cache by the others, while each XCD's concurrent
-    // tiles stay compact (few row-blocks per chunk in its L2)
-    std::vector<std::vector<int>> per(8);
-    for (int r = 0; r < L.R; ++r) {
-        const int q = NT / 8, rem = NT % 8;
-        int j = 0;
-        for (int x = 0; x < 8; ++x) {
-            const int cnt = q + (((x - r) % 8 + 8) % 8 < rem ? 1 : 0);
-            for (int k = 0; k < cnt; ++k, ++j) {
-                per[x].push_back(tiles[j]);
-                per[x].push_back(r);
-            }
-        }
-    }
-    size_t mx = 0;
-    for (auto &v : per) mx = std::max(mx, v.size() / 2);
-    for (size_t sidx = 0; sidx < mx; ++sidx)
-        for (int x = 0; x < 8; ++x) {
-            const bool on = sidx < per[x].size() / 2;
-            L.order.push_back(on ? per[x][2 * sidx] : 0);
-            L.order.push_back(on ? per[x][2 * sidx + 1] : -1);
-        }
-#endif
+    L.tiles = tiles;
+    L.order = i8_sweep_order(tiles, L.R);
     return L;
+}
+
+bool i8_pieces(const I8Layout &L, int k, std::vector<int> &tile_end,
+               std::vector<std::vector<int>> &orders) {
+    // 128-row blocks: weight = the tiles of the block row; every cut is valid
+    const int TI = (L.T64 + 1) / 2;  // 128-row blocks holding rows
+    std::vector<double> w((size_t)TI, 0.0);
+    for (int t : L.tiles) w[(size_t)(t & 0xffff)] += 1.0;
+    std::vector<char> valid((size_t)TI, 1);
+    const std::vector<int> cut = piece_cuts(w, valid, k);
+    if ((int)cut.size() != k - 1) return false;
+    tile_end.clear();
+    orders.clear();
+    int I0 = 0;
+    for (int p = 0; p < k; ++p) {
+        const int I1 = p + 1 < k ? cut[(size_t)p] : TI;
+        std::vector<int> sub;
+        for (int t : L.tiles)
+            if ((t & 0xffff) >= I0 && (t & 0xffff) < I1) sub.push_back(t);
+        orders.push_back(i8_sweep_order(sub, L.R));
+        // the packed upper's 64 x 64 sub-tiles of rows [0, 128 I1): rows of
+        // 64-row blocks b < 2 I1 (clipped to the last block)
+        const int64_t b1 = std::min<int64_t>(2 * (int64_t)I1, L.T64);
+        tile_end.push_back((int)(b1 * L.T64 - b1 * (b1 - 1) / 2));
+        I0 = I1;
+    }
+    return true;
 }
 
 size_t i8_workspace(const I8Layout &L) {
@@ -762,25 +805,31 @@ hipError_t launch_i8_slice(const void *X, int dtype, int64_t ld, int n, int64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables, hipStream_t st) {
+hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables, hipStream_t st,
+                          const void *order_p, int64_t items, const PieceMarks &pm) {
     const I8Ws w = i8_ws(L, ws);
     const int64_t *rb = (const int64_t *)tables;  // {rb (R + 1 int64), order (int pairs)}
-    const int2 *order = (const int2 *)((const char *)tables + (size_t)(L.R + 1) * 8);
-    const int64_t items = (int64_t)L.order.size() / 2;  // one workgroup each
+    const int2 *order = order_p ? (const int2 *)order_p
+                                : (const int2 *)((const char *)tables + (size_t)(L.R + 1) * 8);
+    if (!order_p) items = (int64_t)L.order.size() / 2;  // one workgroup each
+    if (items < 1) return hipSuccess;
     if (L.ns == 2)
         hipLaunchKernelGGL((k_gram_i8<2, I8_NBJ2, BK_I8_W2>), dim3((unsigned)items), dim3(64 * BK_I8_W2), I8_LDS, st, w.S, L.dp,
-                           L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
+                           L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64, pm);
     else
         hipLaunchKernelGGL((k_gram_i8<3, I8_NBJ3, BK_I8_W3>), dim3((unsigned)items), dim3(64 * BK_I8_W3), I8_LDS, st, w.S, L.dp,
-                           L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64);
+                           L.plane, rb, L.R, order, w.es, n, L.T64, w.part, L.ntile64, pm);
     return hipGetLastError();
 }
 
-hipError_t launch_i8_reduce(int64_t d, const I8Layout &L, void *ws, double *U, hipStream_t st) {
+hipError_t launch_i8_reduce(int64_t d, const I8Layout &L, void *ws, double *U, hipStream_t st,
+                            int64_t e0, int64_t e1, bool rec) {
     const I8Ws w = i8_ws(L, ws);
     const int64_t usz = L.ntile64 * 4096;
-    hipLaunchKernelGGL(k_i8_reduce, dim3((unsigned)((usz / 2 + 255) / 256)), dim3(256), 0, st, w.part,
-                       L.R, usz, U, (double)d, w.bound);
+    if (e1 < 0) e1 = usz;
+    if (e1 <= e0) return hipSuccess;
+    hipLaunchKernelGGL(k_i8_reduce, dim3((unsigned)(((e1 - e0) / 2 + 255) / 256)), dim3(256), 0, st,
+                       w.part, L.R, usz, U, (double)d, w.bound, e0, e1, rec ? 1 : 0);
     return hipGetLastError();
 }
 

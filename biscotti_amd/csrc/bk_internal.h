@@ -53,6 +53,35 @@ constexpr int G3_STAGE = G3_MAXB * G3_BLK;                 // 48 KiB
 constexpr int G3_LDS = G3_STAGES * G3_STAGE;               // 144 KiB
 enum { T_NONE = 0, T_OFF = 1, T_PAIR = 2, T_DIAG1 = 3 };
 
+// The exchange overlapped with the Gram (bk_comm_set_mode 2): ONE Gram launch
+// whose workgroups are ordered piece by piece (piece p = launched workgroups
+// [start[p], start[p + 1])); every workgroup, at its exit, counts itself into
+// cnt[p] after an agent-scope release of its partials, and the communication
+// stream waits on the count (hipStreamWaitValue32) before it reduces and
+// all-reduces piece p -- so the pieces' exchanges overlap the later pieces'
+// compute without a launch boundary (and its tail) between the pieces
+struct PieceMarks {
+    unsigned *cnt[8] = {};  // signal memory (hipMallocSignalMemory), one per piece
+    int k = 0;
+    int start[9] = {};
+};
+#ifdef __HIPCC__
+__device__ inline void piece_done(const PieceMarks &pm) {
+    if (pm.k == 0) return;
+    // every storing wave drains its stores (vmcnt 0), the barrier orders them
+    // before thread 0's agent-scope release and count (MI355X_MICROARCH.md,
+    // correctness boundaries: inter-workgroup visibility)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int p = 0;
+        while (p + 1 < pm.k && (int)blockIdx.x >= pm.start[p + 1]) ++p;
+        __threadfence();  // agent scope: the partials reach memory (L2 write-back) before the count
+        atomicAdd(pm.cnt[p], 1u);
+    }
+}
+#endif
+
 struct GroupDesc {
     int nb;               // row-blocks staged (even; padded with a duplicate)
     int blk[G3_MAXB];     // 64-row block index per slot
@@ -97,15 +126,31 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk = G3_BK, int mode = -
 // share of the columns may span two groups: bk_plan.hip "McNaughton")
 hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl,
                         double *part, hipStream_t st, int mode = 0, long long *trace = nullptr,
-                        bool f32_mfma = false);
+                        bool f32_mfma = false, const int *seg = nullptr, int nwg = -1,
+                        const PieceMarks &pm = PieceMarks());
 // fp32 rows for the fp32-MFMA K1 (a distinct element type selects the kernel)
 struct f32m {
     float v;
     __host__ __device__ operator double() const { return v; }
 };
 // f32_mfma: K1 ran on the fp32 MFMA (the record's second trailing element)
+// u0 / u1 / rec: only sub-tiles [u0, u1) (u1 < 0: all), the trailing record
+// written only with rec -- one piece of an exchange overlapped with the Gram
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st,
-                          bool f32_mfma);
+                          bool f32_mfma, int u0 = 0, int u1 = -1, bool rec = true);
+// A split of K1 v3's plan into k launches whose sub-tiles are contiguous
+// pieces [tile_end[p - 1], tile_end[p]) of the packed upper (rows of 64-row
+// blocks), every launched workgroup's segments inside one piece: the same
+// segments and slabs as the one launch, so every sub-tile's sum is bitwise
+// the same.  seg: per piece, 2 ints per launched workgroup (as Plan3Host::seg,
+// the XCD mapping b = 8 j + x kept).  False (k = 1) when the plan has no such
+// split (a workgroup spanning two pieces: the McNaughton plans of n <= 1024)
+bool plan3_pieces(const Plan3Host &H, int k, std::vector<int> &tile_end,
+                  std::vector<std::vector<int>> &seg);
+// the row-block cuts of a k-piece split: weights w[b] of the row blocks,
+// valid[b] whether a cut before block b is allowed; the pieces shrink
+// geometrically (x0.6) so the last exchange, the one left exposed, is small
+std::vector<int> piece_cuts(const std::vector<double> &w, const std::vector<char> &valid, int k);
 hipError_t configure_kernels();
 hipError_t launch_gram(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan &pl,
                        double *part, hipStream_t st);
@@ -193,7 +238,13 @@ struct I8Layout {
     int64_t dp = 0, plane = 0, ntile64 = 0;
     std::vector<int64_t> rb;  // range boundaries (R + 1, multiples of 64 columns)
     std::vector<int> order;   // per workgroup {tile I | J << 16, range (-1: idle)}
+    std::vector<int> tiles;   // the output tiles (I | J << 16), super-blocked
 };
+// k pieces of the tile list by 128-row blocks [I0, I1) (the exchange overlapping
+// the Gram): per piece its workgroup order (as I8Layout::order) and the
+// packed upper's sub-tile range; false when fewer than k cuts exist
+bool i8_pieces(const I8Layout &L, int k, std::vector<int> &tile_end,
+               std::vector<std::vector<int>> &orders);
 I8Layout i8_layout(int n, int64_t d, int es, int num_cu, int ns = 3);
 size_t i8_workspace(const I8Layout &L);
 hipError_t configure_i8_kernels();
@@ -203,8 +254,13 @@ hipError_t configure_i8_kernels();
 // {d, 0, bound, 0}
 hipError_t launch_i8_slice(const void *X, int dtype, int64_t ld, int n, int64_t d,
                            const I8Layout &L, void *ws, const void *tables, hipStream_t st);
-hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables, hipStream_t st);
-hipError_t launch_i8_reduce(int64_t d, const I8Layout &L, void *ws, double *U, hipStream_t st);
+// order / items: one piece's workgroup order (device int pairs), else the layout's
+hipError_t launch_i8_gemm(int n, const I8Layout &L, void *ws, const void *tables, hipStream_t st,
+                          const void *order = nullptr, int64_t items = -1,
+                          const PieceMarks &pm = PieceMarks());
+// [e0, e1) elements of U (e1 < 0: all); the record only with rec
+hipError_t launch_i8_reduce(int64_t d, const I8Layout &L, void *ws, double *U, hipStream_t st,
+                            int64_t e0 = 0, int64_t e1 = -1, bool rec = true);
 
 // bk_small.hip: the whole Multi-Krum of a small batch (n <= 128) in one launch
 struct SmallPlan {

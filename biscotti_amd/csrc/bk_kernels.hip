@@ -795,7 +795,7 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64
                                                   const int *__restrict__ segtab,
                                                   const int *__restrict__ wgtab,
                                                   double *__restrict__ part,
-                                                  long long *__restrict__ trace) {
+                                                  long long *__restrict__ trace, PieceMarks pm) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // debug timeline (BK_TRACE_FILE): per workgroup 100 MHz start/end, shader
@@ -828,6 +828,7 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64
         }
         if (trace) ideal += (long long)(wd[1] < wd[3] ? (wd[3] - 1 - wd[1]) / wd[2] + 1 : 0) * G.cost;
     }
+    piece_done(pm);
     if (trace) {
 #ifdef BK_K1_PROBE
         if (lane == 0) {
@@ -865,13 +866,15 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
                                                  const int *__restrict__ red,
                                                  const int *__restrict__ wglist,
                                                  double *__restrict__ U, int64_t usz,
-                                                 double dcols, double dcols32) {
+                                                 double dcols, double dcols32, int u0, int rec) {
     // the packed upper's two trailing elements: the Gram's column count, and
     // how many of those columns were accumulated at fp32 unit roundoff (the
     // fp32 MFMA); both are summed with the tiles by every exchange, so after
     // one they are totals (K3b's margin: the total d, and u_G = 2^-24 as soon
     // as any shard ran on the fp32 MFMA)
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // (u0 / rec: one piece of the packed upper -- sub-tiles from u0 on, the
+    // record only with the last piece -- when the exchange overlaps the Gram)
+    if (rec && blockIdx.x == 0 && threadIdx.x == 0) {
         U[usz] = dcols;
         U[usz + 1] = dcols32;
         U[usz + 2] = 0.0;  // no int8-sliced columns
@@ -881,7 +884,7 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
     // 64 elements per block, 2 per lane (16-B loads), 8 slabs in flight per
     // sub-list; the same order of adds as below (bitwise the same U)
     __shared__ d2v sub[8][32];
-    const int u = blockIdx.x >> 6, el = threadIdx.x & 31, q = threadIdx.x >> 5;
+    const int u = u0 + (blockIdx.x >> 6), el = threadIdx.x & 31, q = threadIdx.x >> 5;
     const int e = (blockIdx.x & 63) * 64 + el * 2;
     const int off = red[3 * u], np = red[3 * u + 1], slot = red[3 * u + 2];
     const int *wl = wglist + off;
@@ -916,7 +919,7 @@ __global__ __launch_bounds__(256) void k_reduce3(const double *__restrict__ part
     }
 #else
     __shared__ double sub[8][32];
-    const int u = blockIdx.x >> 7, el = threadIdx.x & 31, q = threadIdx.x >> 5;
+    const int u = u0 + (blockIdx.x >> 7), el = threadIdx.x & 31, q = threadIdx.x >> 5;
     const int e = (blockIdx.x & 127) * 32 + el;
     const int off = red[3 * u], np = red[3 * u + 1], slot = red[3 * u + 2];
     const int *wl = wglist + off;
@@ -1960,42 +1963,53 @@ hipError_t launch_synth(void *X, int dtype, int64_t ld, int64_t n, int64_t dl, i
     return hipGetLastError();
 }
 
-hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl,
-                        double *part, hipStream_t st, int mode, long long *trace, bool f32_mfma) {
+hipError_t launch_gram3(const void *X, int dtype, int64_t ld, int n, int64_t d, const Plan3 &pl0,
+                        double *part, hipStream_t st, int mode, long long *trace, bool f32_mfma,
+                        const int *seg, int nwg, const PieceMarks &pm) {
     // mode != 0: timing-only ablations (1: no MFMA, 2: no global loads) -- wrong
     // results, so they exist only in probe builds (-DBK_PROBES); the product ignores mode
     (void)mode;
+    // seg / nwg: one piece's launch table (the exchange overlapping the Gram):
+    // the same segments and slabs, a subset of the launched workgroups
+    Plan3 pl = pl0;
+    if (seg) {
+        pl.d_seg = const_cast<int *>(seg);
+        pl.nwg = nwg;
+    }
+    if (pl.nwg < 1) return hipSuccess;
     const dim3 grid((unsigned)pl.nwg), block(512);
     if (dtype != 0 && f32_mfma)  // fp32 input on the fp32 MFMA
         hipLaunchKernelGGL((k_gram3<0, f32m>), grid, block, G3_LDS, st, (const f32m *)X, ld, n,
-                           pl.nfull, d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
+                           pl.nfull, d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace, pm);
     else if (dtype != 0)  // fp32 input, exact (widened onto the fp64 MFMA): production mode only
         hipLaunchKernelGGL((k_gram3<0, float>), grid, block, G3_LDS, st, (const float *)X, ld, n,
-                           pl.nfull, d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
+                           pl.nfull, d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace, pm);
 #ifdef BK_PROBES
     else if (mode == 1)
         hipLaunchKernelGGL(k_gram3<1>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
-                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
+                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace, pm);
     else if (mode == 2)
         hipLaunchKernelGGL(k_gram3<2>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
-                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
+                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace, pm);
 #endif
     else
         hipLaunchKernelGGL(k_gram3<0>, grid, block, G3_LDS, st, (const double *)X, ld, n, pl.nfull,
-                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace);
+                           d, pl.d_groups, pl.d_seg, pl.d_wg, part, trace, pm);
     return hipGetLastError();
 }
 
 hipError_t launch_reduce3(const double *part, const Plan3 &pl, double *U, hipStream_t st,
-                          bool f32_mfma) {
+                          bool f32_mfma, int u0, int u1, bool rec) {
     const int64_t usz = (int64_t)pl.ntile * 4096;
     const double d32 = f32_mfma ? (double)pl.d : 0.0;
+    if (u1 < 0) u1 = pl.ntile;
+    if (u1 <= u0) return hipSuccess;
 #ifndef BK_REDUCE_V1
-    hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 64), dim3(256), 0, st, part, pl.d_red,
-                       pl.d_wglist, U, usz, (double)pl.d, d32);
+    hipLaunchKernelGGL(k_reduce3, dim3((unsigned)(u1 - u0) * 64), dim3(256), 0, st, part, pl.d_red,
+                       pl.d_wglist, U, usz, (double)pl.d, d32, u0, rec ? 1 : 0);
 #else
-    hipLaunchKernelGGL(k_reduce3, dim3((unsigned)pl.ntile * 128), dim3(256), 0, st, part, pl.d_red,
-                       pl.d_wglist, U, usz, (double)pl.d, d32);
+    hipLaunchKernelGGL(k_reduce3, dim3((unsigned)(u1 - u0) * 128), dim3(256), 0, st, part, pl.d_red,
+                       pl.d_wglist, U, usz, (double)pl.d, d32, u0, rec ? 1 : 0);
 #endif
     return hipGetLastError();
 }

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <array>
 #include <cstdint>
 #include <cstdlib>
@@ -465,6 +466,104 @@ Plan3Host build_plan3(int n, int64_t d, int num_cu, int bk, int mode_in, int rou
         if (seen[u] != 1 || !ok) H.red[3 * u + 1] = -1;  // planner bug marker (checked by the caller)
     H.groups = G;
     return H;
+}
+
+std::vector<int> piece_cuts(const std::vector<double> &w, const std::vector<char> &valid, int k) {
+    // target cumulative fractions: piece p's share of the work proportional
+    // to 0.6^p, so each piece is ~0.6 of the one before (its compute hides
+    // most of the previous piece's exchange) and the last one is small
+    std::vector<int> cuts;
+    const int B = (int)w.size();
+    if (k < 2 || B < 2) return cuts;
+    double tot = 0, wsum = 0, g = 1;
+    for (int p = 0; p < k; ++p, g *= 0.6) wsum += g;
+    for (double x : w) tot += x;
+    std::vector<double> cum((size_t)B + 1, 0.0);
+    for (int b = 0; b < B; ++b) cum[(size_t)b + 1] = cum[(size_t)b] + w[(size_t)b];
+    double acc = 0;
+    g = 1;
+    int prev = 0;
+    for (int p = 0; p + 1 < k; ++p, g *= 0.6) {
+        acc += g / wsum;
+        // the valid cut (strictly after the previous one, leaving room for
+        // the pieces still to come) nearest the target
+        int best = -1;
+        for (int b = prev + 1; b <= B - (k - 1 - p); ++b)
+            if (valid[(size_t)b] && (best < 0 || std::fabs(cum[(size_t)b] / tot - acc) <
+                                                     std::fabs(cum[(size_t)best] / tot - acc)))
+                best = b;
+        if (best < 0) return std::vector<int>();
+        cuts.push_back(best);
+        prev = best;
+    }
+    return cuts;
+}
+
+bool plan3_pieces(const Plan3Host &H, int k, std::vector<int> &tile_end,
+                  std::vector<std::vector<int>> &seg) {
+    const int T = H.T, ng = (int)H.groups.size();
+    // each group's row-block span: the rows of its sub-tiles (OFF tasks (ba <
+    // bb): row ba; PAIR: rows ba and bb; DIAG1: ba)
+    std::vector<int> lo(ng, T), hi(ng, -1);
+    std::vector<double> w((size_t)T, 0.0);
+    for (int g = 0; g < ng; ++g) {
+        const GroupDesc &G = H.groups[g];
+        for (int wv = 0; wv < 8; ++wv) {
+            const int *t = G.task[wv];
+            if (t[0] == T_NONE) continue;
+            int rows[2] = {G.blk[t[1]], t[0] == T_PAIR ? G.blk[t[2]] : -1};
+            for (int r : rows) {
+                if (r < 0) continue;
+                lo[g] = std::min(lo[g], r);
+                hi[g] = std::max(hi[g], r);
+                w[(size_t)r] += t[0] == T_PAIR ? 0.5 * G.cost : G.cost;
+            }
+        }
+    }
+    // a cut before row-block b is valid if no group has rows on both sides
+    std::vector<char> valid((size_t)T, 1);
+    for (int g = 0; g < ng; ++g)
+        for (int b = lo[g] + 1; b <= hi[g]; ++b) valid[(size_t)b] = 0;
+    const std::vector<int> cut = piece_cuts(w, valid, k);
+    if ((int)cut.size() != k - 1) return false;
+    auto piece_of_row = [&](int r) {
+        int p = 0;
+        while (p < k - 1 && r >= cut[(size_t)p]) ++p;
+        return p;
+    };
+    // the launched workgroups by piece, each XCD's list order kept
+    const int nwg = (int)H.seg.size() / 2;
+    std::vector<std::vector<std::vector<int>>> per((size_t)k, std::vector<std::vector<int>>(8));
+    for (int b = 0; b < nwg; ++b) {
+        const int v0 = H.seg[2 * b], cnt = H.seg[2 * b + 1];
+        if (cnt == 0) continue;  // an idle workgroup
+        int p = -1;
+        for (int v = v0; v < v0 + cnt; ++v) {
+            const int g = H.wg[5 * v];
+            const int pg = piece_of_row(lo[g]);
+            if (p >= 0 && pg != p) return false;  // a workgroup spans two pieces
+            p = pg;
+        }
+        per[(size_t)p][(size_t)(b % 8)].push_back(v0);
+        per[(size_t)p][(size_t)(b % 8)].push_back(cnt);
+    }
+    tile_end.clear();
+    seg.clear();
+    for (int p = 0; p < k; ++p) {
+        size_t mx = 0;
+        for (auto &l : per[(size_t)p]) mx = std::max(mx, l.size() / 2);
+        std::vector<int> tb;
+        for (size_t j = 0; j < mx; ++j)
+            for (int x = 0; x < 8; ++x) {
+                const auto &l = per[(size_t)p][(size_t)x];
+                tb.push_back(j < l.size() / 2 ? l[2 * j] : 0);
+                tb.push_back(j < l.size() / 2 ? l[2 * j + 1] : 0);
+            }
+        seg.push_back(tb);
+        const int b1 = p + 1 < k ? cut[(size_t)p] : T;
+        tile_end.push_back(b1 * T - b1 * (b1 - 1) / 2);
+    }
+    return true;
 }
 
 }  // namespace bk

@@ -317,8 +317,10 @@ class Engine:
         buf = ctypes.create_string_buffer(bytes(uid_bytes), _lib.BK_UNIQUE_ID_BYTES)
         check(lib().bk_comm_init(self._ctx, int(nranks), int(rank), buf))
 
-    def comm_set_mode(self, deterministic):
-        check(lib().bk_comm_set_mode(self._ctx, 1 if deterministic else 0))
+    def comm_set_mode(self, mode):
+        """0 (or False): all-reduce; 1 (or True): deterministic all-gather +
+        rank-order sum; 2: all-reduce overlapped with the Gram (bk.h)."""
+        check(lib().bk_comm_set_mode(self._ctx, int(mode)))
 
     def timing_enable(self, on=True):
         check(lib().bk_timing_enable(self._ctx, 1 if on else 0))

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 13
+#define BK_ABI_VERSION 14
 
 typedef struct bk_ctx bk_ctx;
 
@@ -268,8 +268,17 @@ int bk_finish_device(bk_ctx *ctx, const double *d_upper, const void *dX, int dty
 int bk_comm_unique_id(void *id_out /* BK_UNIQUE_ID_BYTES */);
 int bk_comm_init(bk_ctx *ctx, int nranks, int rank, const void *id /* BK_UNIQUE_ID_BYTES */);
 /* 0: ncclAllReduce(sum) of the packed Gram (default);
- * 1: deterministic -- ncclAllGather of the partials + fixed rank-order sum. */
-int bk_comm_set_mode(bk_ctx *ctx, int deterministic);
+ * 1: deterministic -- ncclAllGather of the partials + fixed rank-order sum;
+ * 2: the all-reduce overlapped with the Gram -- the packed upper cut into
+ *    pieces by rows (BK_OVERLAP_PIECES, 2..8, default 2, each ~0.6 of the one
+ *    before), each piece computed by its own launches and all-reduced on a
+ *    communication stream while the next computes.  Every output is bitwise
+ *    mode 0's (the pieces run the same segments / (tile, range) items; the
+ *    sum is element-wise).  Applies where the Gram splits into such pieces
+ *    (K1i8, and the K1 plans whose workgroups each stay in one piece: n >=
+ *    ~2048, config E); elsewhere (config D's n = 512 plan) mode 0 runs.
+ * Set on every rank alike. */
+int bk_comm_set_mode(bk_ctx *ctx, int mode);
 /* Partial Gram of the local column shard -> all-reduce -> scores/selection
  * (redundant on every rank) -> mean of the local columns.  Async on stream. */
 /* d_local = 0 is allowed (an empty trailing shard: dX_local, ld and
@@ -486,7 +495,11 @@ enum bk_kernel_id {
     BK_K_SMALL = 15,     /* K1..K4 fused in one launch for n <= 128 (k_small)   */
     BK_K_SLICE = 16,     /* K1i8 digit slicing + error bound (BK_F32_I8)        */
     BK_K_SCORE_GATHER = 17, /* C2 RCCL all-gather of the split scores (n >= 2049) */
-    BK_NUM_KERNELS = 18
+    /* bk_comm_set_mode 2: from the end of the last Gram piece to the end of
+     * the last all-reduce -- the exchange time the overlap left exposed
+     * (BK_K_ALLREDUCE is then the span from the first all-reduce's start) */
+    BK_K_EXCHANGE_EXPOSED = 18,
+    BK_NUM_KERNELS = 19
 };
 int bk_timing_enable(bk_ctx *ctx, int on);   /* all kernels; clears accumulated timings */
 /* Time only the kernels whose bit (1u << kernel_id) is set: every timed kernel

@@ -41,10 +41,10 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_names():
     L = _lib.lib()
-    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 13
+    assert L.bk_abi_version() == _lib.BK_ABI_VERSION == 14
     assert L.bk_kernel_name(0) == b"k_gram"
     assert L.bk_kernel_name(99) == b"?"
-    assert len(_lib.KERNELS) == 18
+    assert len(_lib.KERNELS) == 19
     for i, name in enumerate(_lib.KERNELS):
         assert L.bk_kernel_name(i) == name.encode()
 
