@@ -666,6 +666,146 @@ def rows_entry_variant(eng, dev, name, calls=None, thread_sweep=(1, 2, 4, 8)):
     return res
 
 
+# §8(f) row 4: each call's dominant dispatch and, for the latency-bound one,
+# its per-workgroup critical path inputs (bench roni_cases' shapes)
+RONI_DOMINANT = {"k_roni": "k_roni_sign", "k_roni_softmax": "k_roni_logits",
+                 "k_roni_softmax_batches": "k_roni_batch"}
+
+
+def roni_roofline(name, ms, meta):
+    """What binds a §8(f) row 4 kernel, from the rocprofv3
+    record of this very libbk.so build (profiles/pmc_roni.json, written by
+    tools/roni_pmc_summary.py; ignored when the library hash differs): the
+    dominant dispatch's busiest resource (MFMA pipe, VALU, LDS or HBM, as a
+    busy fraction) and frac = that fraction, the share of the time the
+    binding resource works; for a latency-bound dispatch (every busy fraction
+    low, waves parked most of the time) the one-launch floor instead: the
+    empty-dispatch floor of the same trace plus the workgroup's critical path,
+    and frac = floor / this launch's time."""
+    path = os.path.join(REPO, "profiles", "pmc_roni.json")
+    dom = RONI_DOMINANT[name]
+    out = {"kernel": dom}
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return dict(out, bound=None, note="no profiles/pmc_roni.json")
+    if rec.get("libbk_sha16") != lib_sha16():
+        return dict(out, bound=None, note="stale: profiles/pmc_roni.json is from another libbk.so")
+    k = rec["kernels"].get(dom, {})
+    busy = {r: k.get(f) for r, f in (("mfma", "mfma_busy"), ("valu", "valu_busy"),
+                                      ("lds", "lds_busy"), ("hbm", "hbm_frac"))}
+    out.update({"busy": {r: (round(v, 4) if v is not None else None) for r, v in busy.items()},
+                "waves_parked": k.get("wait_frac"), "waves_per_cu": k.get("waves_per_cu"),
+                "dispatch_us_profiled": k.get("us_median"), "source": rec.get("source")})
+    top, res_ = max(((v, r) for r, v in busy.items() if v is not None), default=(None, None))
+    if name == "k_roni_softmax_batches":
+        # one workgroup per update (100 of 256 CUs): the floor of one launch is
+        # the empty dispatch plus one workgroup's critical path -- its logit
+        # chains read x and w (fp32) from LDS, 8 B per FMA on each of the
+        # 2 nb C active threads (LDS: 128 B per cycle per CU), and each chain
+        # is d_in + 1 dependent FMAs (>= 4 cycles each)
+        clk = (k.get("clock_ghz") or 2.1) * 1e9
+        lds_cyc = meta["threads"] * (meta["d_in"] + 1) * 8.0 / 128.0
+        chain_cyc = (meta["d_in"] + 1) * 4.0
+        floor_us = (rec.get("launch_floor_us") or 0.0) + max(lds_cyc, chain_cyc) / clk * 1e6
+        out.update({"bound": "latency (one launch)", "floor_us": round(floor_us, 2),
+                    "frac": round(floor_us * 1e-3 / ms, 4),
+                    "floor": "empty dispatch %.2f us + per-workgroup LDS-fed FMA chain %.2f us"
+                             % (rec.get("launch_floor_us") or 0.0,
+                                max(lds_cyc, chain_cyc) / clk * 1e6)})
+        return out
+    out.update({"bound": res_, "unit": "busy fraction of the binding resource", "peak": 1.0,
+                "achieved": round(top, 4) if top is not None else None,
+                "frac": round(top, 4) if top is not None else None})
+    return out
+
+
+def launch_floor_ms(dev, reps=200):
+    """The box's floor for a one-launch kernel, measured as libbk times its
+    kernels (two HIP events around each launch): a 1-workgroup torch kernel
+    (a 1-element add) between events, averaged -- what an empty launch costs
+    on the same clock, the floor a latency-bound single launch approaches;
+    and the back-to-back period of the same launch (dispatch throughput)."""
+    import torch
+    x = torch.zeros(1, device=dev)
+    for _ in range(10):
+        x.add_(1.0)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for a, b in evs:
+        a.record()
+        x.add_(1.0)
+        b.record()
+    torch.cuda.synchronize()
+    each = sum(a.elapsed_time(b) for a, b in evs) / reps
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        x.add_(1.0)
+    b.record()
+    torch.cuda.synchronize()
+    return {"evented_each_ms": round(each, 5), "back_to_back_ms": round(a.elapsed_time(b) / reps, 5)}
+
+
+def roni_cases(eng, dev):
+    """SURVEY §8(f) row 4's kernels on bench-sized inputs: {name: (launch,
+    algorithmic bytes or None, what)} -- K7 (logistic RONI over a
+    creditcard-test-sized set), K8 over the whole set, and K8 with the
+    reference's last-mini-batch semantics (tools/roni_probe.py profiles them)."""
+    import torch
+    runs = {}
+    # RONI (§8(f) row 4): a creditcard-test-sized validation set (30% of
+    # 284,807 rows, d = 25: utils.py:86-117) scoring 512 updates in one launch
+    from biscotti_amd._lib import check, lib
+    nv, dr, nr = 85_000, 25, 512
+    g2 = torch.Generator(device=dev).manual_seed(5)
+    Xv = torch.randn((nv, dr), dtype=torch.float64, device=dev, generator=g2)
+    yv = torch.where(torch.randn(nv, dtype=torch.float64, device=dev, generator=g2) > 0, 1.0, -1.0)
+    ww = torch.randn(dr, dtype=torch.float64, device=dev, generator=g2)
+    dl = torch.randn((nr, dr), dtype=torch.float64, device=dev, generator=g2) * 1e-2
+    rs = torch.empty(nr, dtype=torch.float64, device=dev)
+    runs["k_roni"] = (lambda: check(lib().bk_roni_device(eng.ctx, Xv.data_ptr(), nv, dr, dr,
+                                                         yv.data_ptr(), ww.data_ptr(),
+                                                         dl.data_ptr(), nr, dr, rs.data_ptr())),
+                      None, "RONI scores of %d updates on a %d x %d validation set "
+                            "(logistic_validator.py:22-33)" % (nr, nv, dr),
+                      {"flops": 2.0 * nv * (nr + 1) * dr, "updates": nr})  # nv x (n+1) x d
+    # the torch-path RONI (K8, the mnist softmax verifier, ML/Pytorch/client_obj.py:100-112):
+    # a 6,000-sample shard of 784 fp32 pixels, 10 classes, 100 updates of 7,850
+    nvm, dinm, cm, nrm = 6000, 784, 10, 100
+    Xm = torch.randn((nvm, dinm), dtype=torch.float32, device=dev, generator=g2)
+    ym = torch.randint(0, cm, (nvm,), dtype=torch.int32, device=dev, generator=g2)
+    wm = torch.randn(cm * (dinm + 1), dtype=torch.float64, device=dev, generator=g2) * 0.05
+    dm = torch.randn((nrm, cm * (dinm + 1)), dtype=torch.float64, device=dev, generator=g2) * 1e-3
+    rsm = torch.empty(nrm, dtype=torch.float64, device=dev)
+    ntm = torch.empty(2 * nrm + 1, dtype=torch.int32, device=dev)
+    runs["k_roni_softmax"] = (
+        lambda: check(lib().bk_roni_softmax_device(eng.ctx, Xm.data_ptr(), nvm, dinm, dinm,
+                                                   ym.data_ptr(), cm, wm.data_ptr(), dm.data_ptr(),
+                                                   nrm, cm * (dinm + 1), rsm.data_ptr(),
+                                                   ntm.data_ptr())),
+        None, "softmax RONI scores of %d updates (d = %d), every evaluation over the whole "
+              "%d x %d fp32 set, %d classes (ML/Pytorch/client_obj.py:100-112 with batch_size "
+              ">= nv)" % (nrm, cm * (dinm + 1), nvm, dinm, cm),
+        {"flops": 2.0 * nvm * (nrm + 1) * cm * dinm, "updates": nrm})  # nv x (n+1) x C x d_in
+    # the reference's own semantics (client.py:136-144): each update's original and
+    # after errors on two random last mini-batches of batch_size 10 (honest.go:47)
+    nbm = 10
+    im = torch.randint(0, nvm, (nrm, 2, nbm), dtype=torch.int64, device=dev, generator=g2)
+    runs["k_roni_softmax_batches"] = (
+        lambda: check(lib().bk_roni_softmax_batches_device(
+            eng.ctx, Xm.data_ptr(), nvm, dinm, dinm, ym.data_ptr(), cm, wm.data_ptr(),
+            dm.data_ptr(), nrm, cm * (dinm + 1), im.data_ptr(), nbm, rsm.data_ptr(),
+            ntm.data_ptr())),
+        nrm * cm * (dinm + 1) * 8 + 2 * nrm * nbm * dinm * 4 + cm * (dinm + 1) * 8,
+        "softmax RONI of %d updates (d = %d), each on its two last mini-batches of %d "
+        "samples (client.py:136-144)" % (nrm, cm * (dinm + 1), nbm),
+        {"flops": 2.0 * 2 * nrm * nbm * cm * dinm, "updates": nrm, "workgroups": nrm,
+         "threads": 2 * nbm * cm, "d_in": dinm})
+    return runs
+
+
 def next_rows(eng, X, n, d, sel, m, steps=5):
     """SURVEY.md §8(f) rows 2-4 on the same device-resident batch (HBM-bound):
     block aggregation of the m selected rows into GlobalW (K4'), the
@@ -700,52 +840,10 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
                     "NoisedDelta = Delta + mean of %d noise vectors, %d updates "
                     "(main.go:1524-1537, 1606-1653)" % (k, rows)),
     }
-    # RONI (§8(f) row 4): a creditcard-test-sized validation set (30% of
-    # 284,807 rows, d = 25: utils.py:86-117) scoring 512 updates in one launch
-    from biscotti_amd._lib import check, lib
-    nv, dr, nr = 85_000, 25, 512
-    g2 = torch.Generator(device=dev).manual_seed(5)
-    Xv = torch.randn((nv, dr), dtype=torch.float64, device=dev, generator=g2)
-    yv = torch.where(torch.randn(nv, dtype=torch.float64, device=dev, generator=g2) > 0, 1.0, -1.0)
-    ww = torch.randn(dr, dtype=torch.float64, device=dev, generator=g2)
-    dl = torch.randn((nr, dr), dtype=torch.float64, device=dev, generator=g2) * 1e-2
-    rs = torch.empty(nr, dtype=torch.float64, device=dev)
-    runs["k_roni"] = (lambda: check(lib().bk_roni_device(eng.ctx, Xv.data_ptr(), nv, dr, dr,
-                                                         yv.data_ptr(), ww.data_ptr(),
-                                                         dl.data_ptr(), nr, dr, rs.data_ptr())),
-                      None, "RONI scores of %d updates on a %d x %d validation set "
-                            "(logistic_validator.py:22-33)" % (nr, nv, dr))
-    # the torch-path RONI (K8, the mnist softmax verifier, ML/Pytorch/client_obj.py:100-112):
-    # a 6,000-sample shard of 784 fp32 pixels, 10 classes, 100 updates of 7,850
-    nvm, dinm, cm, nrm = 6000, 784, 10, 100
-    Xm = torch.randn((nvm, dinm), dtype=torch.float32, device=dev, generator=g2)
-    ym = torch.randint(0, cm, (nvm,), dtype=torch.int32, device=dev, generator=g2)
-    wm = torch.randn(cm * (dinm + 1), dtype=torch.float64, device=dev, generator=g2) * 0.05
-    dm = torch.randn((nrm, cm * (dinm + 1)), dtype=torch.float64, device=dev, generator=g2) * 1e-3
-    rsm = torch.empty(nrm, dtype=torch.float64, device=dev)
-    ntm = torch.empty(2 * nrm + 1, dtype=torch.int32, device=dev)
-    runs["k_roni_softmax"] = (
-        lambda: check(lib().bk_roni_softmax_device(eng.ctx, Xm.data_ptr(), nvm, dinm, dinm,
-                                                   ym.data_ptr(), cm, wm.data_ptr(), dm.data_ptr(),
-                                                   nrm, cm * (dinm + 1), rsm.data_ptr(),
-                                                   ntm.data_ptr())),
-        None, "softmax RONI scores of %d updates (d = %d), every evaluation over the whole "
-              "%d x %d fp32 set, %d classes (ML/Pytorch/client_obj.py:100-112 with batch_size "
-              ">= nv)" % (nrm, cm * (dinm + 1), nvm, dinm, cm))
-    # the reference's own semantics (client.py:136-144): each update's original and
-    # after errors on two random last mini-batches of batch_size 10 (honest.go:47)
-    nbm = 10
-    im = torch.randint(0, nvm, (nrm, 2, nbm), dtype=torch.int64, device=dev, generator=g2)
-    runs["k_roni_softmax_batches"] = (
-        lambda: check(lib().bk_roni_softmax_batches_device(
-            eng.ctx, Xm.data_ptr(), nvm, dinm, dinm, ym.data_ptr(), cm, wm.data_ptr(),
-            dm.data_ptr(), nrm, cm * (dinm + 1), im.data_ptr(), nbm, rsm.data_ptr(),
-            ntm.data_ptr())),
-        nrm * cm * (dinm + 1) * 8 + 2 * nrm * nbm * dinm * 4 + cm * (dinm + 1) * 8,
-        "softmax RONI of %d updates (d = %d), each on its two last mini-batches of %d "
-        "samples (client.py:136-144)" % (nrm, cm * (dinm + 1), nbm))
+    runs.update(roni_cases(eng, dev))
     res = {}
-    for name, (fn, nbytes, what) in runs.items():
+    for name, spec in runs.items():
+        fn, nbytes, what = spec[:3]
         fn()
         torch.cuda.synchronize()
         eng.timing_enable(True)
@@ -755,17 +853,15 @@ def next_rows(eng, X, n, d, sel, m, steps=5):
         t = eng.timing_read().get("k_roni" if name.startswith("k_roni") else name)
         eng.timing_enable(False)
         ms = t["avg_ms"]
-        if name.startswith("k_roni") and nbytes is None:  # fp64 MFMA GEMMs: algorithmic flops
-            if name == "k_roni_softmax":  # nv x (n+1) x C x d_in
-                fl, nu = 2.0 * nvm * (nrm + 1) * cm * dinm, nrm
-            else:  # nv x (n+1) x d
-                fl, nu = 2.0 * nv * (nr + 1) * dr, nr
-            res[name] = {"what": what, "ms": round(ms, 4),
-                         "updates_per_s": round(nu / (ms * 1e-3), 1),
-                         "fp64_tflops": round(fl / (ms * 1e-3) / 1e12, 3),
-                         "roofline": {"bound": "mfma", "peak": 78.6, "unit": "TFLOP/s",
-                                      "frac": round(fl / (ms * 1e-3) / 1e12 / 78.6, 4),
-                                      "note": "whole launch (weights prep, GEMM, count, score)"}}
+        if name.startswith("k_roni"):  # §8(f) row 4: what binds, from the PMC record
+            meta = spec[3]
+            fl, nu = meta["flops"], meta["updates"]
+            r = {"what": what, "ms": round(ms, 4), "updates_per_s": round(nu / (ms * 1e-3), 1),
+                 "fp64_tflops_algorithmic": round(fl / (ms * 1e-3) / 1e12, 3)}
+            if nbytes:
+                r["bytes"] = nbytes
+            r["roofline"] = roni_roofline(name, ms, meta)
+            res[name] = r
             continue
         gbs = nbytes / (ms * 1e-3) / 1e9
         res[name] = {"what": what, "ms": round(ms, 4), "bytes": nbytes, "GB_per_s": round(gbs, 1),

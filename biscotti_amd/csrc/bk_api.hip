@@ -236,6 +236,7 @@ struct bk_ctx {
     int test_split_fail = 0;   // BK_TEST_SPLIT_FAIL=p: under BK_TEST_SPLIT_SCORES, share p - 1 "fails"
     int64_t emu_split_n = -1;  // emulation: the n whose other chunks are scored
     DevBuf sgather;            // the gathered scores: parts x chunk doubles
+    DevBuf pcnt;               // the overlapped exchange's per-piece arrival counts
     // bk_comm_set_mode 2: the exchange overlapped with the Gram in this many
     // pieces (BK_OVERLAP_PIECES, default 2; 0: off), all-reduced on cstream
     int overlap = 0;
@@ -283,7 +284,7 @@ void bind_epoch(bk_ctx *c) {
                       &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                       &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
                       &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws,
-                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws, &c->sgather};
+                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws, &c->sgather, &c->pcnt};
     for (DevBuf *b : bufs) b->epoch = &c->ws_epoch;
 }
 
@@ -1807,7 +1808,7 @@ void bk_destroy(bk_ctx *c) {
                           &c->roni_X, &c->roni_y, &c->roni_w, &c->roni_d, &c->roni_cnt, &c->roni_s,
                           &c->noise, &c->diag, &c->bnd, &c->Ut, &c->small_ctr, &c->small_part,
                           &c->mean_part, &c->status, &c->rmc_X, &c->rmc_y, &c->rmc_ws,
-                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws, &c->sgather};
+                      &c->rmc_xn, &c->rmc_idx, &c->rmc_nt, &c->i8ws, &c->sgather, &c->pcnt};
         if (c->hmargin) (void)hipHostFree(c->hmargin);
         if (c->hout) (void)hipHostFree(c->hout);
         if (c->copy) (void)hipStreamSynchronize(c->copy);
@@ -2227,6 +2228,7 @@ int bk_comm_set_mode(bk_ctx *c, int mode) {
 namespace {
 // the communication stream of the overlapped exchange and its events (once)
 int ensure_comm_stream(bk_ctx *c) {
+    CHK(ensure(c->pcnt, 8 * sizeof(unsigned)));
     if (c->cstream) return BK_OK;
     // one signal-memory allocation per piece count (HIP hands signal memory
     // out 8 bytes at a time)
@@ -2236,8 +2238,13 @@ int ensure_comm_stream(bk_ctx *c) {
             HIPCHK(hipExtMallocWithFlags(&sp, 8, hipMallocSignalMemory));
             c->sigcnt[i] = (unsigned *)sp;
         }
+    // the highest stream priority: as Gram workgroups retire, the early
+    // pieces' reduce and all-reduce workgroups are dispatched ahead of the
+    // Gram's remaining ones, so the exchange overlaps the Gram, not its tail
     hipStream_t cs = nullptr;
-    HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+    HIPCHK(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi));
     hipError_t e = hipSuccess;
     hipEvent_t ev[9] = {};
     for (int i = 0; i < 9 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
@@ -2275,7 +2282,8 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
     pl.T = (int)((n + 63) / 64);
     pl.ntile = pl.T * (pl.T + 1) / 2;
     PieceMarks pm;
-    for (int p = 0; p < k; ++p) pm.cnt[p] = c->sigcnt[p];
+    pm.cnt = (unsigned *)c->pcnt.p;
+    for (int p = 0; p < k; ++p) pm.sig[p] = c->sigcnt[p];
     pm.k = k;
     int tot = 0;
     for (int p = 0; p < k; ++p) {
@@ -2299,6 +2307,10 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
         const hipError_t e = hipMemsetAsync(c->sigcnt[p], 0, 8, c->stream);
         if (e != hipSuccess) st = fail(BK_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
     }
+    if (st == BK_OK) {
+        const hipError_t e = hipMemsetAsync(c->pcnt.p, 0, 8 * sizeof(unsigned), c->stream);
+        if (e != hipSuccess) st = fail(BK_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+    }
     if (st == BK_OK && c->test_fail_piece)  // test knob BK_TEST_FAIL_PIECE (bk_create)
         st = fail(BK_EHIP, "test knob BK_TEST_FAIL_PIECE=%d: the Gram fails before its launch",
                   c->test_fail_piece);
@@ -2311,6 +2323,12 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
     // of the order alone; timing only)
     const bool nomark = probe_env("BK_PIECES_NOMARK") != nullptr;
     if (nomark) pm.k = 0;
+    // probe build, timing only (wrong results): BK_PIECES_NOWT=1 -- counts
+    // without write-through stores; BK_PIECES_NOCSTREAM=1 -- counts and
+    // write-through stores, but the communication stream neither reduces nor
+    // all-reduces the early pieces
+    if (probe_env("BK_PIECES_NOWT")) pm.nowt = 1;
+    const bool nocs = probe_env("BK_PIECES_NOCSTREAM") != nullptr;
     if (st == BK_OK) {
         st = timed(c, BK_K_GRAM, [&] {
             return e8 ? launch_i8_gemm((int)n, e8->L, c->i8ws.p, e8->tables, c->stream, pc.d, tot, pm)
@@ -2348,16 +2366,20 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
     // workgroups are done; the last piece (and the record) on the context
     // stream after the Gram, all-reduced there too once the communication
     // stream's all-reduces are done -- one stream hop at the end, not two
+    const bool nowait = probe_env("BK_PIECES_NOWAIT") != nullptr;  // probe: no wait, no early work
     for (int p = 0; p + 1 < k; ++p) {
-        if (launched) {
-            HIPCHK(hipStreamWaitValue32(c->cstream, c->sigcnt[p], (uint32_t)pc.nwg[(size_t)p],
-                                        hipStreamWaitValueGte, 0xffffffffu));
-            HIPCHK(reduce_piece(p, c->cstream, false));
-        }
         if (p == 0 && t_ar) {
             CHK(get_event(c, &ar_a));
             HIPCHK(hipEventRecord(ar_a, c->cstream));
         }
+        if (nowait) continue;
+        if (launched) {
+            HIPCHK(hipStreamWaitValue32(c->cstream, c->sigcnt[p], 1u, hipStreamWaitValueGte,
+                                        0xffffffffu));
+            if (nocs) continue;
+            HIPCHK(reduce_piece(p, c->cstream, false));
+        }
+        if (nocs && launched) continue;
         const int64_t e0 = pc.e[(size_t)p], e1 = pc.e[(size_t)p + 1];
         RCCLCHK(ncclAllReduce(U + e0, U + e0, (size_t)(e1 - e0), ncclDouble, ncclSum, c->comm,
                               c->cstream));

@@ -338,6 +338,7 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
     // this workgroup's item: its tile (row block I of 128, column block J of
     // TJ: I | J << 16) and column range (i8_layout; r < 0: a padding workgroup
     // of a short XCD list)
+    const bool wt = piece_handed(pm) && !pm.nowt;  // the partials go to the communication stream
     const int2 item = order[blockIdx.x];
     if (item.y < 0) {
         piece_done(pm);
@@ -534,8 +535,9 @@ void k_gram_i8(const int8_t *__restrict__ S, int64_t dp, int64_t plane,
                     sh = -19;
                 }
                 const int64_t u = (int64_t)bi * T64 - (int64_t)bi * (bi - 1) / 2 + (bj - bi);
-                part[((int64_t)r * ntile64 + u) * 4096 + (gi & 63) * 64 + (gj & 63)] =
-                    (ei == I8_NONFINITE || ej == I8_NONFINITE) ? __builtin_nan("") : ldexp(v, ei + ej + sh);
+                st_part(&part[((int64_t)r * ntile64 + u) * 4096 + (gi & 63) * 64 + (gj & 63)],
+                        (ei == I8_NONFINITE || ej == I8_NONFINITE) ? __builtin_nan("") : ldexp(v, ei + ej + sh),
+                        wt);
             }
         }
     piece_done(pm);

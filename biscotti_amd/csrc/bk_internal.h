@@ -61,24 +61,48 @@ enum { T_NONE = 0, T_OFF = 1, T_PAIR = 2, T_DIAG1 = 3 };
 // all-reduces piece p -- so the pieces' exchanges overlap the later pieces'
 // compute without a launch boundary (and its tail) between the pieces
 struct PieceMarks {
-    unsigned *cnt[8] = {};  // signal memory (hipMallocSignalMemory), one per piece
+    unsigned *cnt = nullptr;  // device memory: one arrival count per piece (zeroed per call)
+    unsigned *sig[8] = {};    // signal memory (hipMallocSignalMemory): piece p done -> 1
     int k = 0;
     int start[9] = {};
+    int nowt = 0;             // probe build only (BK_PIECES_NOWT): plain stores -- timing A/B, invalid
 };
 #ifdef __HIPCC__
+// Only the pieces before the last are handed to the communication stream
+// (the last is reduced behind the Gram on its own stream): their workgroups
+// store their partials write-through (sc1) and count themselves -- the
+// guide's write-through hand-off (MI355X_MICROARCH.md, correctness
+// boundaries; the form k_small uses): every storing wave drains its sc1
+// stores (vmcnt 0), a workgroup barrier, then one lane's relaxed agent-scope
+// add on the piece's device counter; the workgroup whose add returns the
+// piece's count - 1 saw every other one's drained stores, and raises the
+// piece's signal word (one system-scope store) for the communication
+// stream's hipStreamWaitValue32.  No release fence (a buffer_wbl2 writes back
+// the XCD's whole dirty L2, ~6.5 us), and no per-workgroup atomic on the
+// signal word itself: those serialised at ~0.15-0.3 us each and cost
+// 0.25-0.3 ms per Gram (r6 A/B, tools/ab_overlap.py).
+__device__ inline bool piece_handed(const PieceMarks &pm) {
+    return pm.k > 1 && (int)blockIdx.x < pm.start[pm.k - 1];
+}
 __device__ inline void piece_done(const PieceMarks &pm) {
-    if (pm.k == 0) return;
-    // every storing wave drains its stores (vmcnt 0), the barrier orders them
-    // before thread 0's agent-scope release and count (MI355X_MICROARCH.md,
-    // correctness boundaries: inter-workgroup visibility)
-    __builtin_amdgcn_s_waitcnt(0);
+    if (!piece_handed(pm)) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         int p = 0;
         while (p + 1 < pm.k && (int)blockIdx.x >= pm.start[p + 1]) ++p;
-        __threadfence();  // agent scope: the partials reach memory (L2 write-back) before the count
-        atomicAdd(pm.cnt[p], 1u);
+        const unsigned n_p = (unsigned)(pm.start[p + 1] - pm.start[p]);
+        if (__hip_atomic_fetch_add(pm.cnt + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            n_p - 1u)
+            __hip_atomic_store(pm.sig[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+// a partial's store: write-through (sc1) in a handed-off piece, plain otherwise
+__device__ __forceinline__ void st_part(double *p, double v, bool wt) {
+    if (wt)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
 }
 #endif
 

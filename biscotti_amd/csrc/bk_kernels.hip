@@ -413,21 +413,23 @@ __device__ __forceinline__ void g3_load_rows(d2v (&a)[4], const T *__restrict__ 
     }
 }
 
+// (wt: write-through stores, a piece handed to the communication stream --
+// bk_internal.h piece_done)
 template <typename T = double>
 __device__ __forceinline__ void store_tile(double *out, const typename G3T<T>::acc (&acc)[4][4],
-                                           int rr, int g) {
+                                           int rr, int g, bool wt = false) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                out[(i * 16 + g3_crow<T>(g, r)) * 64 + j * 16 + rr] = (double)acc[i][j][r];
+                st_part(&out[(i * 16 + g3_crow<T>(g, r)) * 64 + j * 16 + rr], (double)acc[i][j][r], wt);
 }
 
 template <typename T, bool SKIP = false>
 __device__ __forceinline__ void store_diag(double *out, const typename G3T<T>::acc (&acc)[10],
-                                           int rr, int g) {
+                                           int rr, int g, bool wt = false) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -435,8 +437,8 @@ __device__ __forceinline__ void store_diag(double *out, const typename G3T<T>::a
             if (SKIP && i == 0 && j == 3) continue;  // written by the OFF wave that took it
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                out[(i * 16 + g3_crow<T>(g, r)) * 64 + j * 16 + rr] =
-                    j >= i ? (double)acc[dix(i, j)][r] : 0.0;
+                st_part(&out[(i * 16 + g3_crow<T>(g, r)) * 64 + j * 16 + rr],
+                        j >= i ? (double)acc[dix(i, j)][r] : 0.0, wt);
         }
 }
 
@@ -497,7 +499,7 @@ template <typename T, int KIND, int MODE, bool STAG, int NB, int XT = 0>
 __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int n, int nfull,
                                         int64_t d, const GroupDesc &G, const int *wd, char *lds,
                                         int wave, int lane, double *out, long long (&probe)[2],
-                                        double *xout = nullptr) {
+                                        double *xout = nullptr, bool wt = false) {
     constexpr int XO = KIND == T_OFF ? XT : 0;     // OFF: extra block side
     constexpr bool XP = KIND == T_PAIR && XT != 0;  // PAIR: skip block (0,3)
     typedef typename G3T<T>::gran gran;
@@ -724,16 +726,17 @@ __device__ __forceinline__ void g3_wave(const T *__restrict__ X, int64_t ld, int
             }
         }
         if constexpr (KIND == T_OFF) {
-            store_tile<T>(out, acc.a, rr, g);
+            store_tile<T>(out, acc.a, rr, g, wt);
             if constexpr (XO != 0) {  // block (0,3) of the PAIR wave's diagonal tile
 #pragma unroll
-                for (int r = 0; r < 4; ++r) xout[g3_crow<T>(g, r) * 64 + 48 + rr] = (double)xacc[r];
+                for (int r = 0; r < 4; ++r)
+                    st_part(&xout[g3_crow<T>(g, r) * 64 + 48 + rr], (double)xacc[r], wt);
             }
         } else if constexpr (KIND == T_PAIR) {
-            store_diag<T, XP>(out, acc.a, rr, g);
-            store_diag<T, XP>(out + 4096, acc.b, rr, g);
+            store_diag<T, XP>(out, acc.a, rr, g, wt);
+            store_diag<T, XP>(out + 4096, acc.b, rr, g, wt);
         } else {
-            store_diag<T>(out, acc.a, rr, g);
+            store_diag<T>(out, acc.a, rr, g, wt);
         }
     }
 }
@@ -745,7 +748,7 @@ template <typename T, int MODE, int NB>
 __device__ __forceinline__ void g3_dispatch(const T *__restrict__ X, int64_t ld, int n,
                                             int nfull, int64_t d, const GroupDesc &G,
                                             const int *wd, char *lds, int wave, int lane,
-                                            double *out, long long (&probe)[2]) {
+                                            double *out, long long (&probe)[2], bool wt) {
     // the balanced quads always stage 4 row-blocks: only NB = 4 (and the
     // run-time NB = 0 of the ablation modes) carries the XT variants
     const int xt = (NB == 4 || NB == 0) ? G.xt[wave] : 0;
@@ -760,31 +763,31 @@ __device__ __forceinline__ void g3_dispatch(const T *__restrict__ X, int64_t ld,
 #endif
         if (wave >= 4 && G3_STAGGER && (!G3T<T>::F32C || BK_F32_STAGGER)) {
             if (xt == 1)
-                g3_wave<T, T_OFF, MODE, true, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+                g3_wave<T, T_OFF, MODE, true, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout, wt);
             else if (xt == 2)
-                g3_wave<T, T_OFF, MODE, true, NB, (NB == 4 || NB == 0) ? 2 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+                g3_wave<T, T_OFF, MODE, true, NB, (NB == 4 || NB == 0) ? 2 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout, wt);
             else
-                g3_wave<T, T_OFF, MODE, true, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+                g3_wave<T, T_OFF, MODE, true, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, nullptr, wt);
         } else {
             if (xt == 1)
-                g3_wave<T, T_OFF, MODE, false, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+                g3_wave<T, T_OFF, MODE, false, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout, wt);
             else if (xt == 2)
-                g3_wave<T, T_OFF, MODE, false, NB, (NB == 4 || NB == 0) ? 2 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout);
+                g3_wave<T, T_OFF, MODE, false, NB, (NB == 4 || NB == 0) ? 2 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, xout, wt);
             else
-                g3_wave<T, T_OFF, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+                g3_wave<T, T_OFF, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, nullptr, wt);
         }
         break;
     case T_PAIR:
         if (xt)
-            g3_wave<T, T_PAIR, MODE, false, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+            g3_wave<T, T_PAIR, MODE, false, NB, (NB == 4 || NB == 0) ? 1 : 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, nullptr, wt);
         else
-            g3_wave<T, T_PAIR, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+            g3_wave<T, T_PAIR, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, nullptr, wt);
         break;
     case T_DIAG1:
-        g3_wave<T, T_DIAG1, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        g3_wave<T, T_DIAG1, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, nullptr, wt);
         break;
     default:
-        g3_wave<T, T_NONE, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+        g3_wave<T, T_NONE, MODE, false, NB>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, nullptr, wt);
         break;
     }
 }
@@ -806,6 +809,7 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64
         t_mt0 = (long long)__builtin_amdgcn_s_memtime();
     }
     long long probe[2] = {0, 0};
+    const bool wt = piece_handed(pm) && !pm.nowt;  // this workgroup's slabs go to the communication stream
     const int v0 = segtab[2 * blockIdx.x], nseg = segtab[2 * blockIdx.x + 1];
     long long ideal = 0;  // sum of nk * cost over the segments (trace only)
     for (int sg = 0; sg < nseg; ++sg) {
@@ -816,15 +820,15 @@ __global__ __launch_bounds__(512, 2) void k_gram3(const T *__restrict__ X, int64
         if (sg > 0) __syncthreads();  // the previous segment's waves are done with the LDS ring
         if constexpr (MODE == 0) {
             switch (G.nb) {
-            case 1: g3_dispatch<T, MODE, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-            case 2: g3_dispatch<T, MODE, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-            case 3: g3_dispatch<T, MODE, 3>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-            case 4: g3_dispatch<T, MODE, 4>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-            case 5: g3_dispatch<T, MODE, 5>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
-            default: g3_dispatch<T, MODE, 6>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe); break;
+            case 1: g3_dispatch<T, MODE, 1>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, wt); break;
+            case 2: g3_dispatch<T, MODE, 2>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, wt); break;
+            case 3: g3_dispatch<T, MODE, 3>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, wt); break;
+            case 4: g3_dispatch<T, MODE, 4>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, wt); break;
+            case 5: g3_dispatch<T, MODE, 5>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, wt); break;
+            default: g3_dispatch<T, MODE, 6>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, wt); break;
             }
         } else {
-            g3_dispatch<T, MODE, 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe);
+            g3_dispatch<T, MODE, 0>(X, ld, n, nfull, d, G, wd, lds, wave, lane, out, probe, wt);
         }
         if (trace) ideal += (long long)(wd[1] < wd[3] ? (wd[3] - 1 - wd[1]) / wd[2] + 1 : 0) * G.cost;
     }

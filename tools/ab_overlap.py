@@ -32,13 +32,17 @@ def main():
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     bootstrap_rccl(eng, 0, 1, lambda b, src: b)
     for rep in range(reps):
-        for mode in ("i8x2_certified", "mfma", "exact"):
-            for label, xm, nomark in (("serial", 0, False), ("overlap", 2, False),
-                                      ("order_only", 2, True)):
-                if nomark:
-                    os.environ["BK_PIECES_NOMARK"] = "1"
-                else:
-                    os.environ.pop("BK_PIECES_NOMARK", None)
+        for mode in sys.argv[3].split(",") if len(sys.argv) > 3 else ("i8x2_certified", "mfma", "exact"):
+            for label, xm, knob in (("serial", 0, None), ("overlap", 2, None),
+                                    ("order_only", 2, "BK_PIECES_NOMARK"),
+                                    ("counts_no_wt", 2, "BK_PIECES_NOWT"),
+                                    ("wait_only", 2, "BK_PIECES_NOCSTREAM"),
+                                    ("counts_no_wait", 2, "BK_PIECES_NOWAIT")):
+                for kn in ("BK_PIECES_NOMARK", "BK_PIECES_NOWT", "BK_PIECES_NOCSTREAM",
+                           "BK_PIECES_NOWAIT"):
+                    os.environ.pop(kn, None)
+                if knob:
+                    os.environ[knob] = "1"
                 v = bench.sharded_variant(eng, dev, "E_4096x262144_fp32", mode, nparts, 0, 1,
                                           lambda: None, nparts, steps=20, warmup=5,
                                           exchange_mode=xm)
@@ -47,7 +51,6 @@ def main():
                                   "k_gram_ms": pr["k_gram_ms"], "exchange_ms": pr["exchange_ms"],
                                   "exposed_ms": pr.get("exchange_exposed_ms"),
                                   "kernels": v["kernels_ms_avg"]}), flush=True)
-    os.environ.pop("BK_PIECES_NOMARK", None)
     eng.close()
 
 
