@@ -155,7 +155,9 @@ def main():
                                                       pmc_k1["tcc_hit_pct"], pmc_k1["mfma_busy_pct"],
                                                       "%.2f" % pmc_k1["clock_ghz"] if pmc_k1["clock_ghz"]
                                                       else "n/a (kernel shorter than the counter window)")]
-    k1 = next((k for k in res if k.startswith(K1_NAMES)), None)
+    # the PMC passes' dominant kernel; else the first K1-family name (the
+    # trace pass also holds e.g. the host-row entries' k_tiny / k_small)
+    k1 = k1p if k1p in res else next((k for k in res if k.startswith(K1_NAMES)), None)
     out_json = {"workload": workload, "source": prof, "kernels": res}
     if k1:
         out_json["k_gram"] = dict(res[k1])
@@ -164,8 +166,10 @@ def main():
         tr = os.path.join(prof, "trace", "run_kernel_trace.csv")
         if len(sys.argv) > 5 and os.path.exists(tr):
             w, st = int(sys.argv[4]), int(sys.argv[5])
-            durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-                    for r in csv.DictReader(open(tr)) if short(r["Kernel_Name"]) == k1]
+            # in dispatch order (the CSV's rows are not always in time order)
+            rows = sorted((r for r in csv.DictReader(open(tr)) if short(r["Kernel_Name"]) == k1),
+                          key=lambda r: int(r["Start_Timestamp"]))
+            durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
             win = durs[w:w + st]
             if win:
                 res[k1]["dispatch_ms"] = durs
