@@ -2238,13 +2238,11 @@ int ensure_comm_stream(bk_ctx *c) {
             HIPCHK(hipExtMallocWithFlags(&sp, 8, hipMallocSignalMemory));
             c->sigcnt[i] = (unsigned *)sp;
         }
-    // the highest stream priority: as Gram workgroups retire, the early
-    // pieces' reduce and all-reduce workgroups are dispatched ahead of the
-    // Gram's remaining ones, so the exchange overlaps the Gram, not its tail
+    // normal priority: a highest-priority stream was measured slower in every
+    // form (two-digit certified 1.38 -> 1.77 ms, fp32 MFMA 4.39 -> 5.12 ms at
+    // E's 8-rank shard)
     hipStream_t cs = nullptr;
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-    HIPCHK(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi));
+    HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     hipError_t e = hipSuccess;
     hipEvent_t ev[9] = {};
     for (int i = 0; i < 9 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
