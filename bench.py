@@ -668,7 +668,7 @@ def rows_entry_variant(eng, dev, name, calls=None, thread_sweep=(1, 2, 4, 8)):
 
 # §8(f) row 4: each call's dominant dispatch and, for the latency-bound one,
 # its per-workgroup critical path inputs (bench roni_cases' shapes)
-RONI_DOMINANT = {"k_roni": "k_roni_sign", "k_roni_softmax": "k_roni_logits",
+RONI_DOMINANT = {"k_roni": "k_roni_sign_reg", "k_roni_softmax": "k_roni_logits",
                  "k_roni_softmax_batches": "k_roni_batch"}
 
 

@@ -166,77 +166,92 @@ __device__ inline bool softmax_near_tie(const float *lg, int C, int best, double
     return !fin || !(l1 - l2 - u * (__builtin_fabs(l1) + __builtin_fabs(l2)) > ea + emax);
 }
 
-// |x_s| for every sample: a workgroup stages 64 samples x 64 features through
-// LDS (coalesced), then thread s sums its row's squares in k order -- the
-// oracle's sequential sum, bit for bit (every fp32 square is exact in fp64)
+// |x_s| for every sample, bit for bit the oracle's sequential sum of squares
+// in k order (every fp32 square is exact in fp64).  The sum is one dependent
+// fp64 add per feature, so the kernel's floor is that chain plus one load
+// round trip: a workgroup takes 16 samples (375 workgroups for 6,000), all 256
+// threads stage a 16 x 512 chunk through LDS with every load in flight (the
+// next chunk's issued before this one is summed), thread s < 16 adds its
+// sample's squares in k order.  (r4f: 64 samples per workgroup and 64-feature
+// chunks loaded one after another: 94 workgroups, 47 us at 6,000 x 784.)
+constexpr int XN_S = 16, XN_KC = 512, XN_PT = XN_S * XN_KC / 256;
 __global__ __launch_bounds__(256) void k_roni_xnorm(const float *__restrict__ Xv, int64_t nv,
                                                     int64_t din, int64_t ldv,
                                                     double *__restrict__ xn) {
-    __shared__ float t[64][65];
+    __shared__ float t[XN_S][XN_KC + 1];
     const int tid = threadIdx.x;
-    const int64_t s0 = (int64_t)blockIdx.x * 64;
-    double acc = 0.0;
-    for (int64_t k0 = 0; k0 < din; k0 += 64) {
-        __syncthreads();
+    const int64_t s0 = (int64_t)blockIdx.x * XN_S;
+    float v[XN_PT];
+    auto load = [&](int64_t k0) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int r = (tid >> 6) + 4 * u, kk = tid & 63;
+        for (int u = 0; u < XN_PT; ++u) {
+            const int i = tid + 256 * u, r = i / XN_KC, kk = i % XN_KC;
             const int64_t sr = s0 + r < nv ? s0 + r : nv - 1;
-            t[r][kk] = k0 + kk < din ? Xv[sr * ldv + k0 + kk] : 0.0f;
+            v[u] = k0 + kk < din ? Xv[sr * ldv + k0 + kk] : 0.0f;
+        }
+    };
+    double acc = 0.0;
+    load(0);
+    for (int64_t k0 = 0; k0 < din; k0 += XN_KC) {
+        __syncthreads();  // the previous chunk has been summed
+#pragma unroll
+        for (int u = 0; u < XN_PT; ++u) {
+            const int i = tid + 256 * u;
+            t[i / XN_KC][i % XN_KC] = v[u];
         }
         __syncthreads();
-        if (tid < 64) {
-            // 16 values read together, then added in k order (r4c read one and
-            // waited for it before every add of the chain)
-            const int kn = (int)(din - k0 < 64 ? din - k0 : 64);
+        if (k0 + XN_KC < din) load(k0 + XN_KC);
+        if (tid < XN_S) {
+            const int kn = (int)(din - k0 < XN_KC ? din - k0 : XN_KC);
             int kk = 0;
             for (; kk + 16 <= kn; kk += 16) {
-                float v[16];
+                float q[16];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = t[tid][kk + u];
+                for (int u = 0; u < 16; ++u) q[u] = t[tid][kk + u];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) acc += (double)v[u] * (double)v[u];
+                for (int u = 0; u < 16; ++u) acc += (double)q[u] * (double)q[u];
             }
             for (; kk < kn; ++kk) {
-                const double v = (double)t[tid][kk];
-                acc += v * v;
+                const double q = (double)t[tid][kk];
+                acc += q * q;
             }
         }
     }
-    if (tid < 64 && s0 + tid < nv) xn[s0 + tid] = __builtin_sqrt(acc);
+    if (tid < XN_S && s0 + tid < nv) xn[s0 + tid] = __builtin_sqrt(acc);
 }
 
 // |w_col| of every model-class column of Wt (the fp32 weights widened), k in
-// order: the oracle's sequential sum.  A workgroup takes 64 columns: all 256
-// threads load a 64-row chunk of them (coalesced rows, every load in flight,
-// the next chunk's issued before this one is summed), thread c < 64 adds its
-// column's 64 values in k order from LDS.  (r4c: one thread per column
-// looping over k with a global load per add, 4 workgroups for 1,010 columns.)
+// order: the oracle's sequential sum.  A workgroup takes 16 columns (one
+// 128-B run of each row): all 256 threads load a 256-row chunk of them with
+// every load in flight (the next chunk's issued before this one is summed),
+// thread c < 16 adds its column's values in k order from LDS.  (r4f: 64
+// columns per workgroup, 16 workgroups for 1,024 columns: 19 us at d = 784.)
+constexpr int WN_C = 16, WN_KC = 256, WN_PT = WN_C * WN_KC / 256;
 __global__ __launch_bounds__(256) void k_roni_wnorm(const double *__restrict__ Wt, int64_t ldl,
                                                     int64_t din, double *__restrict__ wn) {
-    __shared__ double t[64][65];
+    __shared__ double t[WN_KC][WN_C + 1];
     const int tid = threadIdx.x;
-    const int64_t c0 = (int64_t)blockIdx.x * 64;
-    const int cc = tid & 63, r0 = tid >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * WN_C;
+    const int cc = tid % WN_C, r0 = tid / WN_C;  // 16 rows per pass of the workgroup
     const int64_t col = c0 + cc < ldl ? c0 + cc : ldl - 1;
-    double v[16];
+    double v[WN_PT];
     auto load = [&](int64_t k0) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int64_t k = k0 + r0 + 4 * u;
+        for (int u = 0; u < WN_PT; ++u) {
+            const int64_t k = k0 + r0 + (256 / WN_C) * u;
             v[u] = k < din ? Wt[k * ldl + col] : 0.0;
         }
     };
     double acc = 0.0;
     load(0);
-    for (int64_t k0 = 0; k0 < din; k0 += 64) {
+    for (int64_t k0 = 0; k0 < din; k0 += WN_KC) {
         __syncthreads();  // the previous chunk has been summed
 #pragma unroll
-        for (int u = 0; u < 16; ++u) t[r0 + 4 * u][cc] = v[u];
+        for (int u = 0; u < WN_PT; ++u) t[r0 + (256 / WN_C) * u][cc] = v[u];
         __syncthreads();
-        if (k0 + 64 < din) load(k0 + 64);
-        if (tid < 64) {
-            const int kn = (int)(din - k0 < 64 ? din - k0 : 64);
+        if (k0 + WN_KC < din) load(k0 + WN_KC);
+        if (tid < WN_C) {
+            const int kn = (int)(din - k0 < WN_KC ? din - k0 : WN_KC);
             int kk = 0;
             for (; kk + 16 <= kn; kk += 16) {
                 double q[16];
@@ -248,7 +263,7 @@ __global__ __launch_bounds__(256) void k_roni_wnorm(const double *__restrict__ W
             for (; kk < kn; ++kk) acc += t[kk][tid] * t[kk][tid];
         }
     }
-    if (tid < 64 && c0 + tid < ldl) wn[c0 + tid] = __builtin_sqrt(acc);
+    if (tid < WN_C && c0 + tid < ldl) wn[c0 + tid] = __builtin_sqrt(acc);
 }
 
 constexpr int RG_MT = 64, RG_NT = 128, RG_LT = RG_NT + 1;
@@ -516,6 +531,118 @@ __global__ __launch_bounds__(256) void k_roni_sign(const double *__restrict__ Xv
     }
 }
 
+// K7' for d <= 32 (the creditcard verifier: d = 25), r6: every wave works
+// alone -- no LDS, no barriers.  A wave owns 64 model columns and walks `per`
+// blocks of 32 samples: its B fragments (all <= 8 k-steps x 4 column blocks)
+// are loaded once into registers, each sample block's A fragments and labels
+// straight from global memory into registers, issued as soon as the previous
+// block's MFMAs have read theirs.
+// The same fragments, the same v_mfma_f64_16x16x4_f64 chain over k ascending
+// from +0.0 and the same epilogue as k_roni_sign: bitwise the same counts.
+// (k_roni_sign at creditcard shape: 113 us, MFMA busy 34 %, two workgroups per
+// CU by LDS, a barrier pair per tile; profiles/r06/pmc_roni_r06.md.)
+constexpr int RSR_S = 8;  // k-steps of 4: d <= 32
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_roni_sign_reg(const double *__restrict__ Xv, int64_t nv,
+                                                       int64_t din, int64_t ldv,
+                                                       const double *__restrict__ yv,
+                                                       const double *__restrict__ Wt, int64_t ldl,
+                                                       int64_t nmod, int64_t sblocks, int per,
+                                                       unsigned int *__restrict__ cnt) {
+    const int l = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t cblocks = ldl / 64;
+    const int64_t cb = (w % cblocks) * 64;  // neighbouring waves: the same samples
+    const int64_t sb0 = (w / cblocks) * per;
+    if (sb0 >= sblocks) return;  // whole waves only; nothing below synchronises
+    const int nsb = (int)(sblocks - sb0 < per ? sblocks - sb0 : per);
+    const int S = (int)((din + 3) / 4);
+    const int kq = l >> 4, c16 = l & 15;
+    double bf[RSR_S][4];
+#pragma unroll
+    for (int st = 0; st < RSR_S; ++st)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {  // rows past d are zero in Wt (rmm_rows >= 32)
+            const double w = Wt[(int64_t)(4 * st + kq) * ldl + cb + 16 * bb + c16];
+            bf[st][bb] = st < S ? w : 0.0;
+        }
+    double an[2][RSR_S], yn[8];
+    auto load = [&](int64_t sb) {
+        const int64_t r0 = sb * 32;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            int64_t s = r0 + 16 * a + c16;
+            s = s < nv ? s : nv - 1;
+#pragma unroll
+            for (int st = 0; st < RSR_S; ++st) {  // unconditional loads, then a select
+                const int64_t k = 4 * st + kq;
+                const double x = Xv[s * ldv + (k < din ? k : din - 1)];
+                an[a][st] = k < din ? x : 0.0;
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t s = r0 + 16 * a + kq + 4 * r;
+                yn[4 * a + r] = yv[s < nv ? s : nv - 1];
+            }
+    };
+    unsigned int mis[4] = {0, 0, 0, 0};
+    load(sb0);
+    for (int i = 0; i < nsb; ++i) {
+        d4 acc[2][4];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) acc[a][bb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < RSR_S; ++st) {
+            if (st < S) {
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    acc[0][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[0][st], bf[st][bb], acc[0][bb], 0, 0, 0);
+                    acc[1][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[1][st], bf[st][bb], acc[1][bb], 0, 0, 0);
+                }
+            }
+        }
+        // the next block's fragments land in the same registers once these
+        // MFMAs have read them: their latency runs under the MFMAs in flight
+        // and this block's epilogue (a second buffer would take the wave past
+        // 256 registers, one wave per SIMD)
+        double yc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) yc[q] = yn[q];
+        if (i + 1 < nsb) load(sb0 + i + 1);
+        // D reg r of lane l: sample row (l >> 4) + 4 r of the block, column l & 15
+        const int64_t s0 = (sb0 + i) * 32;
+        bool ok_row[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ok_row[q] = s0 + 16 * (q >> 2) + kq + 4 * (q & 3) < nv;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double y = yc[4 * a + r];
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    // np.sign (0 -> 0, NaN -> NaN) as selects: v * 0 is
+                    // +-0 for v = +-0 (== 0 like np.sign's 0) and NaN for NaN
+                    const double v = acc[a][bb][r];
+                    const double yh = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : v * 0.0);
+                    mis[bb] += (unsigned int)(ok_row[4 * a + r] & !(yh == y));
+                }
+            }
+    }
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+        unsigned int tot = mis[bb];
+        tot += __shfl_xor(tot, 16);
+        tot += __shfl_xor(tot, 32);
+        const int64_t j = cb + 16 * bb + l;
+        if (l < 16 && tot && j < nmod) atomicAdd(&cnt[j], tot);
+    }
+}
+
 double roni_softmax_g(int64_t din) {
     const double u = 0x1p-24, nn = (double)(din + 1);
     return nn * u / (1.0 - nn * u) * (1.0 + 0x1p-10);
@@ -529,7 +656,7 @@ size_t roni_softmax_ws(int64_t n, int64_t din, int64_t nv, int C) {
 
 hipError_t launch_roni_xnorm(const float *Xv, int64_t nv, int64_t din, int64_t ldv, double *xn,
                              hipStream_t st) {
-    hipLaunchKernelGGL(k_roni_xnorm, dim3((unsigned)((nv + 63) / 64)), dim3(256), 0, st, Xv, nv, din,
+    hipLaunchKernelGGL(k_roni_xnorm, dim3((unsigned)((nv + XN_S - 1) / XN_S)), dim3(256), 0, st, Xv, nv, din,
                        ldv, xn);
     return hipGetLastError();
 }
@@ -553,7 +680,7 @@ hipError_t launch_roni_softmax(const float *Xv, int64_t nv, int64_t din, int64_t
     hipLaunchKernelGGL(k_roni_mm_prep<true>, dim3((unsigned)(ldl / 64), (unsigned)((rows + 31) / 32)),
                        dim3(256), 0, st, ww, deltas, ld, din, C, nmod, ldl, rows, Wt, bt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_roni_wnorm, dim3((unsigned)((ldl + 63) / 64)), dim3(256), 0, st, Wt, ldl,
+    hipLaunchKernelGGL(k_roni_wnorm, dim3((unsigned)((ldl + WN_C - 1) / WN_C)), dim3(256), 0, st, Wt, ldl,
                        din, wn);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int64_t nx64 = (nv + RG_MT - 1) / RG_MT, ny64 = ldl / RG_NT;
@@ -797,6 +924,26 @@ hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, con
         const int v = e ? atoi(e) : 0;
         return v >= 1 && v <= 256 ? v : 8;
     }();
+    if (d <= 4 * RSR_S && !probe_env("BK_RONI_LDS")) {
+        // one round of resident waves (2 per SIMD at 256 registers): each
+        // wave walks `per` 32-sample blocks, and the grid never spills into a
+        // second round (2,050 waves for 2,048 slots would double the time)
+        static const int64_t slots = [] {
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                cus <= 0)
+                cus = 256;
+            return (int64_t)cus * 4 * 2;
+        }();
+        const int64_t sblocks = (nv + 31) / 32, cblocks = ldl / 64;
+        const int64_t groups = slots / cblocks > 0 ? slots / cblocks : 1;
+        const int64_t per = (sblocks + groups - 1) / groups;
+        const int64_t waves = cblocks * ((sblocks + per - 1) / per);
+        if ((waves + 3) / 4 > 0x7fffffff) return hipErrorInvalidConfiguration;
+        hipLaunchKernelGGL(k_roni_sign_reg, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Xv, nv, d,
+                           ldv, yv, ws, ldl, nmod, sblocks, (int)per, cnt);
+    } else {
     const int64_t tiles = (nv + RG_MT - 1) / RG_MT, ny = ldl / RG_NT;
     const int64_t per = per_env;
     const int64_t nx64 = (tiles + per - 1) / per;
@@ -804,6 +951,7 @@ hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, con
     const int nx = (int)nx64;
     hipLaunchKernelGGL(k_roni_sign, dim3((unsigned)(nx * ny)), dim3(256), 0, st, Xv, nv, d, ldv, yv,
                        ws, ldl, nmod, nx, (int)per, cnt);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_roni_score, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cnt, n,
                        nv, scores);

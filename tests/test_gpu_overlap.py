@@ -1,7 +1,8 @@
 """The exchange overlapped with the Gram (bk_comm_set_mode 2; VERDICT r5 item
-3): the packed upper in k pieces by rows, each computed by its
-own launches and all-reduced on a communication stream while the next
-computes.  Through libbk's sharded entry on a 1-rank RCCL communicator (one
+3): the packed upper in k pieces by rows, computed by ONE Gram
+launch in piece order, each piece reduced and all-reduced on a communication
+stream (behind a device signal the piece's last workgroup raises) while the
+later pieces compute.  Through libbk's sharded entry on a 1-rank RCCL communicator (one
 GPU): every output -- selection, scores, mean, the margin record -- bitwise
 the serial exchange's (mode 0), in the exact, fp32 MFMA and int8 modes, for
 2..5 pieces, on K1 v3 plans that split (n >= ~2048) and on one that does not

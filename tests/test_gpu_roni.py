@@ -51,7 +51,11 @@ def test_roni_goldens_host_validator(engine, name):
 @pytest.mark.parametrize("nv,d,n", [(200_000, 25, 16), (4096, 25, 512), (3000, 785, 33),
                                     (1, 1, 1), (1025, 1024, 2), (777, 25, 15), (778, 25, 16),
                                     # r3b: no cap on d (the MFMA form keeps no model in LDS)
-                                    (2000, 7850, 9), (513, 3001, 130)])
+                                    (2000, 7850, 9), (513, 3001, 130),
+                                    # r6: the register kernel (d <= 32) at its edges
+                                    # and the LDS kernel just past it
+                                    (5000, 32, 200), (3001, 29, 129), (70, 4, 3),
+                                    (1000, 5, 640), (999, 33, 64), (85_000, 25, 512)])
 def test_roni_vs_oracle(engine, oracle, nv, d, n):
     rng = np.random.default_rng(nv + d + n)
     Xv = np.hstack([np.ones((nv, 1)), rng.standard_normal((nv, d - 1))]) if d > 1 else \

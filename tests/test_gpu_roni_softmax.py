@@ -105,6 +105,11 @@ def test_roni_softmax_reference_goldens(engine, oracle, name):
     (500, 300, 10, 95, {}),
     (300, 129, 16, 63, {}),
     (257, 65, 3, 200, {"nan": True}),
+    # r6 norm kernels: 16 samples / 512 features a chunk (k_roni_xnorm),
+    # 16 columns / 256 features a chunk (k_roni_wnorm), ragged at every edge
+    (17, 513, 10, 3, {}),
+    (33, 1100, 4, 40, {}),
+    (16, 256, 16, 1, {}),
 ])
 def test_roni_softmax_full_set_vs_oracle(engine, oracle, nv, din, C, n, kw):
     X, y, ww, D = _case(nv, din, C, n, nv + din + C + n, **kw)

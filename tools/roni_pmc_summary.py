@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import pmc_summary as P  # noqa: E402
 
 KERNELS = {  # libbk call -> its dispatches
-    "K7 bk_roni (logistic)": ("k_roni_mm_prep<false>", "k_roni_sign", "k_roni_score"),
+    "K7 bk_roni (logistic)": ("k_roni_mm_prep<false>", "k_roni_sign_reg", "k_roni_sign", "k_roni_score"),
     "K8 bk_roni_softmax (one batch)": ("k_roni_xnorm", "k_roni_mm_prep<true>", "k_roni_wnorm",
                                        "k_roni_logits", "k_roni_mc_score"),
     "K8 bk_roni_softmax_batches": ("k_roni_batch",),

@@ -5,18 +5,25 @@ torch kernel launched back to back, timed with events.  Under rocprofv3
 (tools/profile_roni.sh) its dispatches give each kernel's duration and
 counters.
 
-    python tools/roni_probe.py [reps]
+    python tools/roni_probe.py [reps] [--probe]   (--probe: the -DBK_PROBES
+        build, e.g. BK_RONI_LDS=1 for r5's LDS-staged K7 kernel)
 """
 import json
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
     import torch
     import bench
+    if "--probe" in sys.argv:
+        sys.argv.remove("--probe")
+        import probe_build
+        from biscotti_amd import _lib
+        probe_build.use(_lib)
     from biscotti_amd.krum import Engine
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     dev = torch.device("cuda", 0)
