@@ -542,12 +542,13 @@ __global__ __launch_bounds__(256) void k_roni_sign(const double *__restrict__ Xv
 // (k_roni_sign at creditcard shape: 113 us, MFMA busy 34 %, two workgroups per
 // CU by LDS, a barrier pair per tile; profiles/r06/pmc_roni_r06.md.)
 constexpr int RSR_S = 8;  // k-steps of 4: d <= 32
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_roni_sign_reg(const double *__restrict__ Xv, int64_t nv,
+template <int NA>  // 16-sample row blocks per wave block: 2 (2 waves / SIMD) or 1 (3)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA == 1 ? 3 : 2))) void k_roni_sign_reg(const double *__restrict__ Xv, int64_t nv,
                                                        int64_t din, int64_t ldv,
                                                        const double *__restrict__ yv,
                                                        const double *__restrict__ Wt, int64_t ldl,
                                                        int64_t nmod, int64_t sblocks, int per,
-                                                       unsigned int *__restrict__ cnt) {
+                                                       unsigned int *__restrict__ cnt, int abl) {
     const int l = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t cblocks = ldl / 64;
@@ -565,11 +566,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             const double w = Wt[(int64_t)(4 * st + kq) * ldl + cb + 16 * bb + c16];
             bf[st][bb] = st < S ? w : 0.0;
         }
-    double an[2][RSR_S], yn[8];
+    double an[NA][RSR_S], yn[4 * NA];
     auto load = [&](int64_t sb) {
-        const int64_t r0 = sb * 32;
+        const int64_t r0 = sb * 16 * NA;
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
+        for (int a = 0; a < NA; ++a) {
             int64_t s = r0 + 16 * a + c16;
             s = s < nv ? s : nv - 1;
 #pragma unroll
@@ -580,7 +581,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             }
         }
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < NA; ++a)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t s = r0 + 16 * a + kq + 4 * r;
@@ -590,9 +591,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     unsigned int mis[4] = {0, 0, 0, 0};
     load(sb0);
     for (int i = 0; i < nsb; ++i) {
-        d4 acc[2][4];
+        d4 acc[NA][4];
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < NA; ++a)
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb) acc[a][bb] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -600,8 +601,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             if (st < S) {
 #pragma unroll
                 for (int bb = 0; bb < 4; ++bb) {
-                    acc[0][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[0][st], bf[st][bb], acc[0][bb], 0, 0, 0);
-                    acc[1][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[1][st], bf[st][bb], acc[1][bb], 0, 0, 0);
+#pragma unroll
+                    for (int a = 0; a < NA; ++a)
+                        acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[a][st], bf[st][bb], acc[a][bb], 0, 0, 0);
                 }
             }
         }
@@ -609,27 +611,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         // MFMAs have read them: their latency runs under the MFMAs in flight
         // and this block's epilogue (a second buffer would take the wave past
         // 256 registers, one wave per SIMD)
-        double yc[8];
+        double yc[4 * NA];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) yc[q] = yn[q];
-        if (i + 1 < nsb) load(sb0 + i + 1);
+        for (int q = 0; q < 4 * NA; ++q) yc[q] = yn[q];
+        if (i + 1 < nsb && !(abl & 2)) load(sb0 + i + 1);  // abl & 2: timing-only, no reloads
         // D reg r of lane l: sample row (l >> 4) + 4 r of the block, column l & 15
-        const int64_t s0 = (sb0 + i) * 32;
-        bool ok_row[8];
+        const int64_t s0 = (sb0 + i) * 16 * NA;
+        if (abl & 1) {  // timing-only: one compare per accumulator instead of the epilogue
 #pragma unroll
-        for (int q = 0; q < 8; ++q) ok_row[q] = s0 + 16 * (q >> 2) + kq + 4 * (q & 3) < nv;
+            for (int bb = 0; bb < 4; ++bb) mis[bb] += (unsigned int)(acc[0][bb][0] == 1234.5 || acc[NA - 1][bb][3] == 1234.5);
+            continue;
+        }
+        // !(np.sign(v) == y) by the label's class: sign(v) is 1, -1, +-0 or
+        // NaN, so it equals y only for y = 1 and v > 0, y = -1 and v < 0, or
+        // y = +-0 and v = +-0 (any other y, NaN included, never matches).
+        // Three compares per output and lane-mask logic, no selects.
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < NA; ++a)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double y = yc[4 * a + r];
+                const bool ok = s0 + 16 * a + kq + 4 * r < nv;
+                const bool yp = y == 1.0, yn = y == -1.0, yz = y == 0.0;
 #pragma unroll
                 for (int bb = 0; bb < 4; ++bb) {
-                    // np.sign (0 -> 0, NaN -> NaN) as selects: v * 0 is
-                    // +-0 for v = +-0 (== 0 like np.sign's 0) and NaN for NaN
                     const double v = acc[a][bb][r];
-                    const double yh = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : v * 0.0);
-                    mis[bb] += (unsigned int)(ok_row[4 * a + r] & !(yh == y));
+                    const bool match = (yp & (v > 0.0)) | (yn & (v < 0.0)) | (yz & (v == 0.0));
+                    mis[bb] += (unsigned int)(ok & !match);
                 }
             }
     }
@@ -936,13 +944,23 @@ hipError_t launch_roni(const double *Xv, int64_t nv, int64_t d, int64_t ldv, con
                 cus = 256;
             return (int64_t)cus * 4 * 2;
         }();
-        const int64_t sblocks = (nv + 31) / 32, cblocks = ldl / 64;
-        const int64_t groups = slots / cblocks > 0 ? slots / cblocks : 1;
+        const char *na_env = probe_env("BK_RONI_NA");
+        const int na = na_env && atoi(na_env) == 2 ? 2 : 1;
+        const int64_t sblocks = (nv + 16 * na - 1) / (16 * na), cblocks = ldl / 64;
+        int64_t groups = slots * (na == 1 ? 3 : 2) / 2 / cblocks;
+        if (groups < 1) groups = 1;
+        if (const char *g = probe_env("BK_RONI_GROUPS")) groups = atoi(g) > 0 ? atoi(g) : groups;
         const int64_t per = (sblocks + groups - 1) / groups;
+        const char *ab = probe_env("BK_RONI_ABL");  // timing-only ablations (probe build)
+        const int abl = ab ? atoi(ab) : 0;
         const int64_t waves = cblocks * ((sblocks + per - 1) / per);
         if ((waves + 3) / 4 > 0x7fffffff) return hipErrorInvalidConfiguration;
-        hipLaunchKernelGGL(k_roni_sign_reg, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Xv, nv, d,
-                           ldv, yv, ws, ldl, nmod, sblocks, (int)per, cnt);
+        if (na == 1)
+            hipLaunchKernelGGL(k_roni_sign_reg<1>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Xv,
+                               nv, d, ldv, yv, ws, ldl, nmod, sblocks, (int)per, cnt, abl);
+        else
+            hipLaunchKernelGGL(k_roni_sign_reg<2>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Xv,
+                               nv, d, ldv, yv, ws, ldl, nmod, sblocks, (int)per, cnt, abl);
     } else {
     const int64_t tiles = (nv + RG_MT - 1) / RG_MT, ny = ldl / RG_NT;
     const int64_t per = per_env;
