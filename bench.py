@@ -61,9 +61,10 @@ def cpu_model():
 
 
 def lib_sha16():
-    import hashlib
+    """the hash PMC records are matched on: libbk.so's device code
+    (_lib.code_object_sha16), not the whole file"""
     from biscotti_amd import _lib
-    return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
+    return _lib.code_object_sha16()
 
 
 def max_over_ranks(v, dev):
@@ -668,7 +669,7 @@ def rows_entry_variant(eng, dev, name, calls=None, thread_sweep=(1, 2, 4, 8)):
 
 # §8(f) row 4: each call's dominant dispatch and, for the latency-bound one,
 # its per-workgroup critical path inputs (bench roni_cases' shapes)
-RONI_DOMINANT = {"k_roni": "k_roni_sign_reg", "k_roni_softmax": "k_roni_logits",
+RONI_DOMINANT = {"k_roni": "k_roni_sign_reg<1>", "k_roni_softmax": "k_roni_logits",
                  "k_roni_softmax_batches": "k_roni_batch"}
 
 

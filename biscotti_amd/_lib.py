@@ -105,6 +105,32 @@ class BKError(RuntimeError):
         self.status = status
 
 
+def code_object_sha16(path=None):
+    """sha256 (16 hex digits) of libbk.so's device code: its .hip_fatbin
+    section, i.e. the gfx950 code objects of every kernel.  PMC records
+    (profiles/pmc_*.json) are stamped with it, so a record stays valid across
+    host-only rebuilds and goes stale when any kernel's code changes."""
+    import hashlib
+    import struct
+    with open(path or LIB_PATH, "rb") as fh:
+        data = fh.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        raise ValueError("not an ELF64 file: %s" % (path or LIB_PATH))
+    shoff = struct.unpack_from("<Q", data, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def section(i):
+        return struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+
+    stroff = section(shstrndx)[4]
+    for i in range(shnum):
+        name, _, _, _, off, size = section(i)
+        end = data.index(b"\0", stroff + name)
+        if data[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    raise ValueError("no .hip_fatbin section in %s" % (path or LIB_PATH))
+
+
 def lib():
     """Load libbk.so; raise loudly if it has not been built."""
     global _lib

@@ -156,3 +156,24 @@ def test_no_gpu_fails_loudly():
     from biscotti_amd.krum import Engine
     with pytest.raises((RuntimeError, ValueError)):
         Engine(0)
+
+
+def test_code_object_hash_is_the_fatbin(tmp_path):
+    """PMC records are matched on the hash of libbk.so's .hip_fatbin (the
+    kernels' code), which bench.py recomputes; a non-ELF file is refused"""
+    import re
+    from biscotti_amd import _lib
+    h = _lib.code_object_sha16()
+    assert re.fullmatch(r"[0-9a-f]{16}", h)
+    assert bench_lib_sha16() == h
+    bad = tmp_path / "x.so"
+    bad.write_bytes(b"not an elf")
+    with pytest.raises(ValueError):
+        _lib.code_object_sha16(str(bad))
+
+
+def bench_lib_sha16():
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    return importlib.import_module("bench").lib_sha16()

@@ -179,8 +179,9 @@ def main():
                           "timed window (dispatches %d..%d, = bench.py's timed steps): avg %.3f ms"
                           % (w + 1, w + st, sum(win) / len(win))]
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    import hashlib
-    sha = hashlib.sha256(open(os.path.join(repo, "biscotti_amd", "libbk.so"), "rb").read()).hexdigest()[:16]
+    sys.path.insert(0, repo)
+    from biscotti_amd._lib import code_object_sha16
+    sha = code_object_sha16(os.path.join(repo, "biscotti_amd", "libbk.so"))  # the kernels' code
     out_json["libbk_sha16"] = sha
     json.dump(out_json, open(out + ".json", "w"), indent=1)
     if k1 and "hbm_bytes_per_launch" in out_json["k_gram"]:

@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import pmc_summary as P  # noqa: E402
 
 KERNELS = {  # libbk call -> its dispatches
-    "K7 bk_roni (logistic)": ("k_roni_mm_prep<false>", "k_roni_sign_reg", "k_roni_sign", "k_roni_score"),
+    "K7 bk_roni (logistic)": ("k_roni_mm_prep<false>", "k_roni_sign_reg<1>", "k_roni_sign_reg<2>", "k_roni_sign", "k_roni_score"),
     "K8 bk_roni_softmax (one batch)": ("k_roni_xnorm", "k_roni_mm_prep<true>", "k_roni_wnorm",
                                        "k_roni_logits", "k_roni_mc_score"),
     "K8 bk_roni_softmax_batches": ("k_roni_batch",),
@@ -84,10 +84,10 @@ def main():
                 k, f(us), f(mf), f(va), f(ld), f(hbm), f(wait), f(occ), binds))
     lines += ["", "Launch floor (the shortest 1-workgroup dispatch in the same trace): %s us" %
               ("-" if floor_us is None else "%.2f" % floor_us)]
-    import hashlib
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res["libbk_sha16"] = hashlib.sha256(open(os.path.join(repo, "biscotti_amd", "libbk.so"),
-                                             "rb").read()).hexdigest()[:16]
+    sys.path.insert(0, repo)
+    from biscotti_amd._lib import code_object_sha16
+    res["libbk_sha16"] = code_object_sha16(os.path.join(repo, "biscotti_amd", "libbk.so"))  # the kernels' code
     res["source"] = "%s.json (tools/profile_roni.sh)" % os.path.relpath(out, repo)
     with open(out + ".json", "w") as fp:
         json.dump(res, fp, indent=1)
