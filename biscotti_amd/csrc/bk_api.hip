@@ -221,6 +221,11 @@ struct bk_ctx {
     int test_fail_exchange = 0;  // test knob BK_TEST_FAIL_BEFORE_EXCHANGE (bk_create)
     int test_i8_enomem = 0;      // test knob BK_TEST_I8_ENOMEM: K1i8's workspace "fails" (bk_create)
     int test_fail_piece = 0;     // test knob BK_TEST_FAIL_PIECE=p: the overlapped Gram's piece p-1 fails
+    int test_pieces_disagree = 0;  // test knob BK_TEST_PIECES_DISAGREE=1: act as if a peer cut the pieces differently
+    // the overlapped exchange's piece layout as agreed at the signature's first
+    // call: false when the ranks' layouts differed (every rank then exchanges
+    // whole, serially, for that signature)
+    bool overlap_agreed = true;
     // split scoring (stage_finish): at n >= split_min_n each rank of a sharded
     // call scores its share of the rows and the ranks all-gather the scores
     // (BK_SPLIT_SCORES_MIN_N; 0 turns it off).  Knobs for a 1-rank
@@ -1784,6 +1789,7 @@ int bk_create(bk_ctx **out, int device) {
     if (const char *v = getenv("BK_TEST_FAIL_BEFORE_EXCHANGE")) c->test_fail_exchange = atoi(v);
     if (const char *v = getenv("BK_TEST_I8_ENOMEM")) c->test_i8_enomem = atoi(v) != 0;
     if (const char *v = getenv("BK_TEST_FAIL_PIECE")) c->test_fail_piece = atoi(v);
+    if (const char *v = getenv("BK_TEST_PIECES_DISAGREE")) c->test_pieces_disagree = atoi(v);
     if (const char *v = getenv("BK_SPLIT_SCORES_MIN_N")) c->split_min_n = atoll(v);
     if (const char *v = getenv("BK_TEST_SPLIT_SCORES")) c->test_split_scores = atoi(v);
     if (const char *v = getenv("BK_EMU_SPLIT_SCORES")) c->emu_split_scores = atoi(v);
@@ -2207,7 +2213,7 @@ int bk_comm_init(bk_ctx *c, int nranks, int rank, const void *id) {
     }
     // the sharded entry's status agreement word, before the communicator (an
     // allocation failure then fails this rank's init, not a later collective)
-    CHK(ensure(c->status, sizeof(double)));
+    CHK(ensure(c->status, 4 * sizeof(double)));
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof uid);
     RCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
@@ -2441,9 +2447,13 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
                  int64_t f, int64_t *d_sel, double *d_scores, double *d_mean) {
     const int64_t usz = bk_upper_elems(n);
     const bool exch = c->comm != nullptr;
+    // the call's signature, the same on every rank by the API's contract: a
+    // change makes the ranks agree again (status, and the overlapped piece layout)
+    const int sig = c->deterministic + 2 * c->overlap +
+                    32 * (dtype == BK_F32 ? c->f32_mode : c->f64_mode);
     const bool agree = exch && (c->nranks > 1 || c->test_fail_exchange) &&
                        (n != c->agreed_n || f != c->agreed_f || dtype != c->agreed_dtype ||
-                        c->deterministic + 2 * c->overlap != c->agreed_det);
+                        sig != c->agreed_det);
     const ScoreSplit sp = score_split(c, n);
     int prep = ensure(c->U, (size_t)usz * sizeof(double));
     if (prep == BK_OK && exch && c->deterministic)
@@ -2471,12 +2481,28 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
                     c->test_fail_exchange);
     const std::string prep_msg = prep == BK_OK ? std::string() : g_err;
     if (agree) {
+        // one max-all-reduce of {status, piece layout, -piece layout}: the ranks
+        // learn whether any failed, and whether they all cut the Gram into the
+        // same pieces (the layout's fingerprint equal on every rank: max ==
+        // -max(-fp)).  A rank whose plan does not split, or a different cut,
+        // turns the overlapped exchange off on every rank for this signature:
+        // each piece is one collective, so the ranks must agree on them.
         double *w = (double *)c->status.p;
-        double mine = prep == BK_OK ? 0.0 : 1.0, any = 0.0;
-        HIPCHK(hipMemcpyAsync(w, &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
-        RCCLCHK(ncclAllReduce(w, w, 1, ncclDouble, ncclMax, c->comm, c->stream));
-        HIPCHK(hipMemcpyAsync(&any, w, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        double v[3] = {prep == BK_OK ? 0.0 : 1.0, 0.0, 0.0};
+        if (pcs) {
+            uint64_t h = 1469598103934665603ull;
+            auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+            mix((uint64_t)pcs->k);
+            for (int64_t x : pcs->e) mix((uint64_t)x);
+            v[1] = (double)(h >> 12) + 1.0;  // 52 bits: exact in a double, never 0
+        }
+        v[2] = -v[1] - (c->test_pieces_disagree ? 1.0 : 0.0);
+        HIPCHK(hipMemcpyAsync(w, v, sizeof v, hipMemcpyHostToDevice, c->stream));
+        RCCLCHK(ncclAllReduce(w, w, 3, ncclDouble, ncclMax, c->comm, c->stream));
+        HIPCHK(hipMemcpyAsync(v, w, sizeof v, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        const double any = v[0];
+        c->overlap_agreed = v[1] != 0.0 && v[1] == -v[2];
         if (prep != BK_OK) {
             g_err = prep_msg;
             return prep;
@@ -2487,7 +2513,7 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
         c->agreed_n = n;
         c->agreed_f = f;
         c->agreed_dtype = dtype;
-        c->agreed_det = c->deterministic + 2 * c->overlap;
+        c->agreed_det = sig;
     } else if (prep != BK_OK && (!exch || c->U.bytes < (size_t)usz * sizeof(double))) {
         return prep;  // nothing to join (no communicator), or no partial to poison
     }
@@ -2497,6 +2523,7 @@ int sharded_once(bk_ctx *c, const void *dX, int dtype, int64_t n, int64_t dl, in
     pl.T = (int)((n + 63) / 64);
     pl.ntile = pl.T * (pl.T + 1) / 2;
     int st = prep;
+    if (!c->overlap_agreed) pcs = nullptr;  // a peer cut the Gram differently (or not at all)
     if (pcs && st == BK_OK)
         return sharded_overlapped(c, *pcs, dX, dtype, n, dl, ld, f, U, pl, d_sel, d_scores, d_mean,
                                   sp);

@@ -144,3 +144,32 @@ def test_failed_piece_poisons_and_joins(oracle, fail_piece):
         assert ex >= 1
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("disagree", [0, 1])
+def test_piece_layout_agreed_across_ranks(oracle, disagree):
+    """the ranks agree on the piece layout at a signature's first call (one
+    max-all-reduce of {status, layout, -layout}, run here on 1 rank through
+    BK_TEST_FAIL_BEFORE_EXCHANGE=3, which agrees without failing): equal
+    layouts keep the overlapped exchange; a peer that cut differently
+    (BK_TEST_PIECES_DISAGREE=1) turns it off, and the call exchanges whole --
+    bitwise the same either way"""
+    n, d, f = 2500, 4096, 750
+    X = torch.from_numpy(oracle.synth(n, d, 2024, f)).cuda()
+    os.environ["BK_TEST_FAIL_BEFORE_EXCHANGE"] = "3"
+    if disagree:
+        os.environ["BK_TEST_PIECES_DISAGREE"] = "1"
+    try:
+        eng = _engine()
+    finally:
+        os.environ.pop("BK_TEST_FAIL_BEFORE_EXCHANGE", None)
+        os.environ.pop("BK_TEST_PIECES_DISAGREE", None)
+    try:
+        ser = _run(eng, X, f, 0)
+        ovl = _run(eng, X, f, 2, pieces=2)
+        ovl2 = _run(eng, X, f, 2, pieces=2)  # the agreed signature: no new agreement
+    finally:
+        eng.close()
+    assert _same(ser, ovl) and _same(ser, ovl2)
+    for o in (ovl, ovl2):
+        assert ("exchange_exposed" in o[4]) == (not disagree)
