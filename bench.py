@@ -392,8 +392,10 @@ def sharded_variant(eng, dev, name, f32_mode, nparts, rank, world, barrier, emu,
         # later pieces) and the part of it left after the last piece
         ex, sp_ = avg("exchange_exposed"), avg("allreduce")
         mine["exchange_exposed_ms"] = ex
-        mine["overlapped_fraction"] = (round(1.0 - ex / sp_, 4) if ex is not None and sp_
-                                       else None)
+        # clamped at 0: at one rank the span IS the exposed part, and the two
+        # event pairs differ by their own granularity (a few us)
+        mine["overlapped_fraction"] = (round(max(0.0, 1.0 - ex / sp_), 4)
+                                       if ex is not None and sp_ else None)
     per_rank = [mine]
     if world > 1:
         hs, per_rank = [None] * world, [None] * world
