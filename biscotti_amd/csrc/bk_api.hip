@@ -2336,6 +2336,17 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
     // all-reduces the early pieces
     if (probe_env("BK_PIECES_NOWT")) pm.nowt = 1;
     const bool nocs = probe_env("BK_PIECES_NOCSTREAM") != nullptr;
+    // the communication stream starts behind everything queued before the
+    // Gram (the counts' reset, the previous call's finish still reading U) --
+    // NOT behind the Gram itself, whose pieces it takes as they complete
+    // (r6 fix: this record sat after the Gram launch, so the early pieces'
+    // work waited for the whole Gram and nothing overlapped)
+    bool cs_started = false;
+    if (st == BK_OK && !nomark) {
+        HIPCHK(hipEventRecord(c->ev_piece[0], c->stream));
+        HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_piece[0], 0));
+        cs_started = true;
+    }
     if (st == BK_OK) {
         st = timed(c, BK_K_GRAM, [&] {
             return e8 ? launch_i8_gemm((int)n, e8->L, c->i8ws.p, e8->tables, c->stream, pc.d, tot, pm)
@@ -2358,10 +2369,11 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
     }
     const std::string st_msg = st == BK_OK ? std::string() : g_err;
     if (st != BK_OK) CHK(poison_upper(c, U, n));
-    // the communication stream starts behind everything queued so far (the
-    // counts' reset above, or the poisoned record)
-    HIPCHK(hipEventRecord(c->ev_piece[0], c->stream));
-    HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_piece[0], 0));
+    if (!cs_started || !launched) {
+        // no Gram ran: the communication stream starts behind the poisoned record
+        HIPCHK(hipEventRecord(c->ev_piece[0], c->stream));
+        HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_piece[0], 0));
+    }
     hipEvent_t ar_a = nullptr, ar_b = nullptr, ex_a = nullptr, ex_b = nullptr;
     const bool t_ar = timing_on(c, BK_K_ALLREDUCE), t_ex = timing_on(c, BK_K_EXCHANGE_EXPOSED);
     auto reduce_piece = [&](int p, hipStream_t s, bool rec) -> hipError_t {
