@@ -248,7 +248,13 @@ struct bk_ctx {
     hipStream_t cstream = nullptr;
     hipEvent_t ev_piece[8] = {};
     hipEvent_t ev_cdone = nullptr;
-    unsigned *sigcnt[8] = {};       // the pieces' completion counts (signal memory, 8 B each)
+    unsigned *sigcnt[8] = {};       // probe A/B only (BK_PIECES_DEVWAIT): signal memory for hipStreamWaitValue32
+    // the pieces' completion words, polled by the host: fine-grained pinned
+    // host memory, one 64-B line per piece (the Gram's last workgroup of a
+    // piece stores 1 there, system scope)
+    unsigned *hsig = nullptr;       // host address
+    unsigned *hsig_d = nullptr;     // the same words as the device addresses them
+    bool sig_pending = false;       // a launched Gram's piece words not all seen yet
     int wait_value_ok = -1;         // hipDeviceAttributeCanUseStreamWaitValue (-1: not asked)
     int64_t exchanges = 0;        // exchanges of the packed Gram (bk_comm_stats)
     double exchanged_bytes = 0;   // bytes each rank put into them
@@ -1833,6 +1839,7 @@ void bk_destroy(bk_ctx *c) {
         if (c->cstream) (void)hipStreamDestroy(c->cstream);
         for (unsigned *sgc : c->sigcnt)
             if (sgc) (void)hipFree(sgc);
+        if (c->hsig) (void)hipHostFree(c->hsig);
         if (c->rstage) (void)hipHostFree(c->rstage);
         delete c->hpool;
         if (c->copy) (void)hipStreamDestroy(c->copy);
@@ -2239,14 +2246,19 @@ namespace {
 int ensure_comm_stream(bk_ctx *c) {
     CHK(ensure(c->pcnt, 8 * sizeof(unsigned)));
     if (c->cstream) return BK_OK;
-    // one signal-memory allocation per piece count (HIP hands signal memory
-    // out 8 bytes at a time)
-    for (int i = 0; i < 8; ++i)
-        if (!c->sigcnt[i]) {
-            void *sp = nullptr;
-            HIPCHK(hipExtMallocWithFlags(&sp, 8, hipMallocSignalMemory));
-            c->sigcnt[i] = (unsigned *)sp;
+    if (!c->hsig) {
+        void *hp = nullptr, *dp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, 8 * 64, hipHostMallocCoherent));
+        memset(hp, 0, 8 * 64);
+        const hipError_t e = hipHostGetDevicePointer(&dp, hp, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(hp);
+            return fail(BK_EHIP, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
         }
+        c->hsig = (unsigned *)hp;
+        c->hsig_d = (unsigned *)dp;
+    }
+
     // normal priority: a highest-priority stream was measured slower in every
     // form (two-digit certified 1.38 -> 1.77 ms, fp32 MFMA 4.39 -> 5.12 ms at
     // E's 8-rank shard)
@@ -2290,7 +2302,26 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
     pl.ntile = pl.T * (pl.T + 1) / 2;
     PieceMarks pm;
     pm.cnt = (unsigned *)c->pcnt.p;
-    for (int p = 0; p < k; ++p) pm.sig[p] = c->sigcnt[p];
+    // r6: the host polls the piece words and queues each piece's reduce and
+    // all-reduce as it completes.  A hipStreamWaitValue32 on the communication
+    // stream (the probe build's BK_PIECES_DEVWAIT) held a command-processor
+    // wait for the whole Gram and slowed it (E's 8-rank shard, exact: +0.85 ms
+    // for the wait alone)
+    if (probe_env("BK_PIECES_DEVWAIT") && !c->sigcnt[0])
+        for (int i = 0; i < 8; ++i) {  // HIP hands signal memory out 8 bytes at a time
+            void *sp = nullptr;
+            HIPCHK(hipExtMallocWithFlags(&sp, 8, hipMallocSignalMemory));
+            c->sigcnt[i] = (unsigned *)sp;
+        }
+    const bool devwait = probe_env("BK_PIECES_DEVWAIT") != nullptr && c->sigcnt[0];
+    for (int p = 0; p < k; ++p) pm.sig[p] = devwait ? c->sigcnt[p] : c->hsig_d + 16 * p;
+    if (c->sig_pending) {
+        // a previous call's Gram may still store into the words (its host
+        // wait was cut short): let it drain before they are reset
+        (void)hipStreamSynchronize(c->stream);
+        c->sig_pending = false;
+    }
+    for (int p = 0; p < 8; ++p) __atomic_store_n(c->hsig + 16 * p, 0u, __ATOMIC_RELEASE);
     pm.k = k;
     int tot = 0;
     for (int p = 0; p < k; ++p) {
@@ -2310,7 +2341,7 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
     }
     // 1. zero the piece counts; K1i8: the digit slices; then the one Gram launch
     bool launched = false;
-    for (int p = 0; p < k && st == BK_OK; ++p) {
+    for (int p = 0; p < k && st == BK_OK && devwait; ++p) {
         const hipError_t e = hipMemsetAsync(c->sigcnt[p], 0, 8, c->stream);
         if (e != hipSuccess) st = fail(BK_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
     }
@@ -2354,6 +2385,7 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
                                      nullptr, f32m, pc.d, tot, pm);
         });
         launched = st == BK_OK;
+        if (launched && !devwait && !nomark) c->sig_pending = true;
     }
     if (nomark && launched) {
         for (int p = 0; p < k; ++p) {
@@ -2387,14 +2419,35 @@ int sharded_overlapped(bk_ctx *c, const Pieces &pc, const void *dX, int dtype, i
     // stream's all-reduces are done -- one stream hop at the end, not two
     const bool nowait = probe_env("BK_PIECES_NOWAIT") != nullptr;  // probe: no wait, no early work
     for (int p = 0; p + 1 < k; ++p) {
-        if (p == 0 && t_ar) {
-            CHK(get_event(c, &ar_a));
-            HIPCHK(hipEventRecord(ar_a, c->cstream));
+        // the exchange's span starts when piece 0 is done (after its wait), so
+        // span - exposed is the exchange work that ran under the Gram
+        auto span_start = [&]() -> int {
+            if (p == 0 && t_ar && !ar_a) {
+                CHK(get_event(c, &ar_a));
+                HIPCHK(hipEventRecord(ar_a, c->cstream));
+            }
+            return BK_OK;
+        };
+        if (nowait) {
+            CHK(span_start());
+            continue;
         }
-        if (nowait) continue;
-        if (launched) {
+        if (launched && devwait) {
             HIPCHK(hipStreamWaitValue32(c->cstream, c->sigcnt[p], 1u, hipStreamWaitValueGte,
                                         0xffffffffu));
+        } else if (launched) {
+            // until the piece's last workgroup stores its word -- or the
+            // context stream has drained (the Gram done, or failed), which
+            // the stream query below notices
+            const volatile unsigned *w = c->hsig + 16 * p;
+            for (unsigned spin = 1; __atomic_load_n(w, __ATOMIC_ACQUIRE) == 0u; ++spin) {
+                _mm_pause();
+                if ((spin & 1023u) == 0u && hipStreamQuery(c->stream) != hipErrorNotReady) break;
+            }
+            if (p + 2 == k) c->sig_pending = false;  // every word this Gram stores has been seen
+        }
+        CHK(span_start());
+        if (launched) {
             if (nocs) continue;
             HIPCHK(reduce_piece(p, c->cstream, false));
         }

@@ -37,9 +37,10 @@ def main():
                                     ("order_only", 2, "BK_PIECES_NOMARK"),
                                     ("counts_no_wt", 2, "BK_PIECES_NOWT"),
                                     ("wait_only", 2, "BK_PIECES_NOCSTREAM"),
-                                    ("counts_no_wait", 2, "BK_PIECES_NOWAIT")):
+                                    ("counts_no_wait", 2, "BK_PIECES_NOWAIT"),
+                                    ("devwait", 2, "BK_PIECES_DEVWAIT")):
                 for kn in ("BK_PIECES_NOMARK", "BK_PIECES_NOWT", "BK_PIECES_NOCSTREAM",
-                           "BK_PIECES_NOWAIT"):
+                           "BK_PIECES_NOWAIT", "BK_PIECES_DEVWAIT"):
                     os.environ.pop(kn, None)
                 if knob:
                     os.environ[knob] = "1"
