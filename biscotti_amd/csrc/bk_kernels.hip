@@ -1509,6 +1509,9 @@ __global__ __launch_bounds__(1024) void k_compact(const int *__restrict__ mask, 
 // rows [y L, y L + L) into part[y][c] (no divide), k_mean_comb adds the
 // segments in order -- a fixed order that depends on m only, so every shard
 // and device of one call adds alike
+#ifndef BK_MEAN_DEPTH
+#define BK_MEAN_DEPTH 8  // rows' loads in flight per thread (same adds in the same order at any depth)
+#endif
 template <typename T, bool VEC, bool ACCUM = false, bool SEG = false>
 __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t ld, int64_t d,
                                               const int64_t *__restrict__ sel, int m,
@@ -1531,12 +1534,12 @@ __global__ __launch_bounds__(256) void k_mean(const T *__restrict__ X, int64_t l
             d2v acc = {0.0, 0.0};
             if constexpr (ACCUM) acc = d2v{mean[c], mean[c + 1]};
             int r = 0;
-            for (; r + 8 <= m; r += 8) {
-                d2v v[8];
+            for (; r + BK_MEAN_DEPTH <= m; r += BK_MEAN_DEPTH) {
+                d2v v[BK_MEAN_DEPTH];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) v[q] = ld2s<T, VEC>(X + srow[r + q] + c);
+                for (int q = 0; q < BK_MEAN_DEPTH; ++q) v[q] = ld2s<T, VEC>(X + srow[r + q] + c);
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
+                for (int q = 0; q < BK_MEAN_DEPTH; ++q) {
                     acc.x += v[q].x;
                     acc.y += v[q].y;
                 }
